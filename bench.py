@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Benchmark: PageRank rounds/s on R-MAT scale 26 (BASELINE.json config 4) on MI355X.
+
+A "step" is one PageRank round (PageRank.java:92-164): the fused pull SpMV over every
+distinct edge, dangling redistribution and damping, plus -- on more than one GPU -- the RCCL
+all-gather of the contribution vector.  The graph (R-MAT scale 26, edge factor 16, seed 4,
+generated on the device; ~1.06e9 distinct edges) is resident in HBM before timing starts.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--no-cpu-baseline]
+  (N > 1: launched by torch.distributed.run, one process per GPU; RCCL over xGMI; the
+   graph is the same for every N -> strong scaling)
+
+Prints ONE JSON line on rank 0 (metric GTEPS = distinct edges / round time / 1e9).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "page-rank-and-tfidf-using-apache-spark_amd"))
+
+import prmi355x as P  # noqa: E402  (load the engine before torch so it binds ROCm's own HIP)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rounds", type=int, default=2)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(eng, rounds: int):
+    """The oracle's plain-fp64 OpenMP restatement ("port") on this host's cores, timed on a
+    bounded sample: `rounds` rounds over the SAME graph (exported CSR, relabelled)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    rp, col, od, dw = eng.export_csr()
+    info = eng.info()
+    t0 = time.time()
+    res = O.pagerank_csr(rp, col, od, dw, int(info["n_tot"]), rounds, exact=False,
+                         threads=cores)
+    wall = time.time() - t0
+    gteps = info["nnz"] / res["sec_per_iter"] / 1e9
+    return {"value": round(gteps, 4), "unit": "GTEPS", "cores": cores, "kind": "port",
+            "sample": f"{rounds} rounds of the same R-MAT graph ({int(info['nnz'])} edges), "
+                      f"oracle/pagerank_oracle.c fast mode (plain fp64 OpenMP pull), "
+                      f"{res['sec_per_iter']:.3f} s/round, {wall:.1f} s total"}
+
+
+def load_traffic(path: str, workload: str):
+    """Per-launch HBM bytes of the SpMV kernel from the committed rocprofv3 PMC summary."""
+    try:
+        d = json.load(open(path))
+        e = d.get(workload)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if a.gpus != world and world > 1:
+        a.gpus = world
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)   # rendezvous only
+    eng = P.Engine(n_ranks=world, rank=rank)
+    if world > 1:
+        import torch
+        uid = P.comm_unique_id() if rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        eng.comm_init(bytes(t.tolist()))
+    t0 = time.time()
+    eng.generate_rmat(a.scale, a.edge_factor, a.seed)
+    info = eng.info()
+    build_s = time.time() - t0
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    if a.warmup > 0:
+        eng.run(a.warmup)
+    barrier()
+    t1 = time.perf_counter()
+    st = eng.run(a.steps)
+    t2 = time.perf_counter()
+    barrier()
+    wall = t2 - t1
+    if dist is not None:
+        import torch
+        w = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w.item())
+        k = torch.tensor([st["ms_spmv_kernel"]], dtype=torch.float64)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        st["ms_spmv_kernel"] = float(k.item())
+    ms_step = wall * 1e3 / a.steps
+    nnz = int(info["nnz"])
+    n = int(info["n_vertices"])
+    gteps = nnz / (ms_step * 1e-3) / 1e9
+    workload = f"rmat-s{a.scale}-ef{a.edge_factor}"
+    # roofline of the dominant kernel (spmv_round): SURVEY.md 8d bytes, this rank's share
+    local_nnz = int(info["local_nnz"])
+    bytes_launch = 4 * local_nnz + 24 * n // world + 8
+    kms = st["ms_spmv_kernel"]
+    achieved = bytes_launch / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    traffic = load_traffic(a.traffic_json, f"{workload}-p{world}")
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(eng, a.cpu_rounds)
+    if rank == 0:
+        line = {
+            "metric": "PageRank GTEPS per round (distinct edges / round time), R-MAT scale-26",
+            "value": round(gteps, 3),
+            "unit": "GTEPS",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Graph500 R-MAT generated on device, Philox seed %d)" % a.seed,
+            "config": {"workload": workload, "scale": a.scale, "edge_factor": a.edge_factor,
+                       "vertices": n, "distinct_edges": nnz, "rounds_per_step": 1,
+                       "parallelism": f"rows dealt over {world} GPU(s), RCCL all-gather of x"
+                       if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "spmv_round", "kernel_ms": round(kms, 4),
+                         "algorithmic_bytes_per_launch": bytes_launch},
+            "cpu_baseline": cpu,
+            "device_ms_per_round": round(st["ms_per_iter"], 4),
+            "build_s": round(build_s, 2),
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

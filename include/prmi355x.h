@@ -1,0 +1,182 @@
+/*
+ * prmi355x -- MI355X-native PageRank engine: the drop-in C ABI.
+ *
+ * This library replaces the per-iteration hot path of the reference Spark job
+ * (ajak6/Page-Rank-and-TFIDF-using-Apache-Spark, PageRank.java) -- the contribution
+ * flatMapToPair (PageRank.java:94-117), the dangling-mass reduce (:121-138) and the
+ * reduceByKey(Sum) + damping rank update (:139-160) -- together with the graph ingest that
+ * feeds it (:26-83) and the top-K output it drains into (:167-204).  Every entry point
+ * below names the reference code it stands in for.
+ *
+ * Plain C: pointers + sizes only.  All host buffers are caller-allocated; the library owns
+ * device memory until pr_destroy().  A context is NOT thread-safe (one caller thread per
+ * context); calls block until their device work is complete.  Every function returns
+ * PR_OK (0) or a negative PR_E_* code; pr_last_error() holds the message.
+ *
+ * Multi-GPU: one process per GPU.  Each process creates a context with opts.n_ranks /
+ * opts.rank, exchanges the 128-byte id from pr_comm_unique_id() (rank 0) out of band, and
+ * calls pr_comm_init() before ingesting.  Ingest/generation is replicated; every rank keeps
+ * the rows (destination pages) dealt to it.  pr_run / pr_get_ranks / pr_topk /
+ * pr_write_top_page are collective (all ranks call them).
+ */
+#ifndef PRMI355X_H
+#define PRMI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRMI355X_VERSION_MAJOR 0
+#define PRMI355X_VERSION_MINOR 1
+
+/* ---- error codes (reference failure -> code) ---------------------------------------- */
+#define PR_OK 0
+#define PR_E_ARG (-1)            /* bad argument / call order                              */
+#define PR_E_PARSE (-2)          /* line with < 2 tab fields: ArrayIndexOutOfBoundsException
+                                    at PageRank.java:40 (arcs) / :49 (mapping)            */
+#define PR_E_EMPTY_DANGLING (-3) /* danglingMap.values().reduce on an empty RDD:
+                                    UnsupportedOperationException("empty collection"),
+                                    PageRank.java:125                                       */
+#define PR_E_HIP (-4)            /* HIP runtime failure                                     */
+#define PR_E_RCCL (-5)           /* RCCL failure                                            */
+#define PR_E_OOM (-6)            /* host or device allocation failed                        */
+#define PR_E_IO (-7)             /* file open/read/write failed (PageRank.java:201-204)     */
+#define PR_E_NODEV (-8)          /* context created without a device (host-only)           */
+
+/* pr_opts.device special values */
+#define PR_DEVICE_FROM_RANK (-1) /* use opts.rank % visible device count                    */
+#define PR_DEVICE_NONE (-2)      /* host-only context: ingest parses, nothing runs on a GPU */
+
+typedef struct pr_ctx pr_ctx;
+
+/* Replaces the hard-coded job constants of PageRank.java: iteration count (:92),
+ * damping 0.15/0.85 (:143), top-K 100 (:189,:193), output ./topPage (:192). */
+typedef struct {
+  int32_t device;   /* HIP device ordinal, or PR_DEVICE_FROM_RANK / PR_DEVICE_NONE        */
+  int32_t n_ranks;  /* processes (GPUs) sharing the graph; 1 = single GPU                 */
+  int32_t rank;     /* this process's rank, 0 <= rank < n_ranks                           */
+  uint32_t topk;    /* rows written by pr_write_top_page; 100 = reference (:189)          */
+  uint32_t flags;   /* PR_F_* below                                                       */
+  uint32_t reserved[7];
+} pr_opts;
+
+#define PR_F_TRACK_RESIDUAL 0x1u /* compute the exact L1 residual every iteration          */
+#define PR_F_VERBOSE 0x2u        /* phase timings on stderr                                */
+
+typedef struct {
+  int32_t iterations;     /* iterations executed                                          */
+  int32_t failed_iteration; /* 1-based iteration that hit PR_E_EMPTY_DANGLING, else 0    */
+  double ms_total;        /* device time of the whole iteration loop (HIP events)          */
+  double ms_per_iter;
+  double ms_spmv_kernel;  /* average duration of the fused SpMV kernel per iteration       */
+  double gteps;           /* nnz / ms_per_iter                                            */
+  double residual;        /* last relative L1 residual sum|r'-r| / sum r' (if tracked)    */
+  double rank_sum;        /* sum of ranks after the run (exact; if tracked)               */
+  uint64_t nnz;           /* distinct edges of the whole graph                            */
+  uint64_t n_vertices;
+  uint64_t defined;       /* vertices with a defined rank after the run (whole graph)      */
+  uint64_t bytes_per_iter;/* algorithmic bytes per iteration                  */
+  uint64_t reserved[6];
+} pr_stats;
+
+typedef struct {
+  uint64_t n_vertices;    /* dense vertex slots (ids seen in arcs or mapping)             */
+  uint64_t raw_edges;     /* arc lines / generated edges                                  */
+  uint64_t nnz;           /* distinct (src,dst) pairs: distinct() at PageRank.java:42     */
+  uint64_t n_tot;         /* mappingFile.distinct().count(), PageRank.java:60             */
+  uint64_t n_pairs;       /* distinct (id,title) pairs, PageRank.java:51                  */
+  uint64_t dangling_entries; /* |subtractByKey(...).keys()|, PageRank.java:56              */
+  uint64_t n_sources;     /* keys of adjacencyList (outdeg >= 1), PageRank.java:42,76     */
+  uint64_t n_rows;        /* vertices with in-degree >= 1 (whole graph)                   */
+  uint64_t local_rows;    /* rows owned by this rank                                      */
+  uint64_t local_nnz;     /* edges owned by this rank                                     */
+  double ms_ingest;       /* host parse + hashing                                         */
+  double ms_build;        /* device CSR build                                             */
+  uint64_t reserved[6];
+} pr_graph_info;
+
+/* Library version "major.minor". */
+const char* pr_version(void);
+void pr_opts_default(pr_opts* opts);
+
+/* SparkConf + JavaSparkContext (PageRank.java:22-23): binds the device / rank. */
+int pr_create(pr_ctx** out, const pr_opts* opts);
+/* spark.stop()-equivalent: frees device memory and the id table. */
+void pr_destroy(pr_ctx* ctx);
+/* Message of the last failing call on this context ("" if none). */
+const char* pr_last_error(const pr_ctx* ctx);
+
+/* Multi-GPU rendezvous.  Replaces the Spark shuffle transport that moves contributions
+ * between executors (reduceByKey at PageRank.java:139) with RCCL over xGMI. */
+int pr_comm_unique_id(uint8_t id_out[128]);
+int pr_comm_init(pr_ctx* ctx, const uint8_t id[128]);
+
+/* textFile(arcs)/textFile(mapping) + mapToPair(split) + distinct + groupByKey + cache +
+ * subtractByKey + distinct().count() (PageRank.java:26-60), then the device CSR build. */
+int pr_ingest_files(pr_ctx* ctx, const char* arcs_path, const char* mapping_path);
+int pr_ingest_buffers(pr_ctx* ctx, const char* arcs, size_t arcs_len,
+                      const char* mapping, size_t mapping_len);
+
+/* In-memory graph (ids already dense, 0..n-1): the same job on a pre-parsed link list.
+ * mapw[v] = number of distinct titles of v (0 = v absent from the mapping); n_tot as
+ * PageRank.java:60.  mapw may be NULL (every id mapped once, n_tot = n). */
+int pr_load_edges(pr_ctx* ctx, const uint32_t* src, const uint32_t* dst, uint64_t m,
+                  uint32_t n, const uint32_t* mapw, uint64_t n_tot);
+
+/* Synthetic Graph500 R-MAT (a,b,c,d = .57,.19,.19,.05), edge_factor << scale edges,
+ * generated on the device (Philox-4x32-10 keyed by seed and edge index); mapping = every
+ * id 0..2^scale-1 once with title "v<id>", n_tot = 2^scale. */
+int pr_generate_rmat(pr_ctx* ctx, int32_t scale, int32_t edge_factor, uint64_t seed);
+
+int pr_graph_get_info(pr_ctx* ctx, pr_graph_info* out);
+
+/* The loop at PageRank.java:92-164: `iterations` rounds of contribution SpMV + dangling
+ * redistribution + damping.  tol > 0 stops early once the relative L1 residual is <= tol
+ * (implies PR_F_TRACK_RESIDUAL).  Returns PR_E_EMPTY_DANGLING where the reference job
+ * would die at :125 (stats->failed_iteration says which round).  Collective. */
+int pr_run(pr_ctx* ctx, int32_t iterations, double tol, pr_stats* stats);
+
+/* Final `ranks` RDD as a dense array indexed by vertex id (0.0 = no rank: the page is
+ * absent from the reference's ranks RDD).  n must be >= n_vertices.  Collective. */
+int pr_get_ranks(pr_ctx* ctx, double* out, uint64_t n);
+
+/* ranks.join(mappings) -> sortByKey(false) -> take(k) (PageRank.java:167-189).  Writes up
+ * to k rows: pair index (into the distinct (id,title) pairs, see pr_pair), vertex id and
+ * rank, descending by rank; equal ranks ordered by (title bytes, id).  *count = rows
+ * written.  Collective. */
+int pr_topk(pr_ctx* ctx, uint32_t k, uint64_t* pair_out, uint32_t* id_out, double* rank_out,
+            uint32_t* count);
+
+/* FileWriter("./topPage") loop (PageRank.java:190-204): `title \t Double.toString(rank)`
+ * for the top opts.topk rows.  Only rank 0 writes.  Collective. */
+int pr_write_top_page(pr_ctx* ctx, const char* path);
+
+/* Id / title strings (the reference's String keys).  *len = full length; at most cap
+ * bytes copied.  For generated / in-memory graphs the id string is the decimal id. */
+int pr_id_string(pr_ctx* ctx, uint32_t v, char* buf, size_t cap, size_t* len);
+int pr_pair(pr_ctx* ctx, uint64_t i, uint32_t* id, char* title, size_t cap, size_t* len);
+
+/* Structure checks (bit-exact CSR/degree construction): per-vertex out-degree (distinct
+ * out-neighbours, PageRank.java:103-108), in-degree and dangling weight (:56), and an
+ * order-free digest {sum, xor} of mix64(src<<32|dst) over the distinct edge set. */
+int pr_get_degrees(pr_ctx* ctx, uint32_t* outdeg, uint32_t* indeg, uint32_t* dang_w,
+                   uint64_t n);
+int pr_edge_digest(pr_ctx* ctx, uint64_t digest_out[2]);
+
+/* Host copy of the pull CSR in the engine's internal numbering (single-rank contexts):
+ * a square graph over internal ids 0..n-1 -- row_ptr[n+1] by destination, col = source
+ * ids (ascending within a row), out-degree and dangling weight per internal id.  The same
+ * graph relabelled, for external baselines.  Pass NULL buffers to query sizes. */
+int pr_export_csr(pr_ctx* ctx, uint64_t* row_ptr, uint32_t* col, uint32_t* outdeg,
+                  uint32_t* dang_w, uint64_t* n, uint64_t* nnz);
+
+/* Java Double.toString layout (PageRank.java:197 string concatenation). Returns length. */
+int pr_format_double(double v, char* buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRMI355X_H */

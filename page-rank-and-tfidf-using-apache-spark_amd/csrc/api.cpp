@@ -1,0 +1,676 @@
+// prmi355x C ABI (include/prmi355x.h): host runtime around the device engine.
+//
+// One context = one process = one GPU.  The round loop of PageRank.java:92-164 runs here:
+// per round one fused SpMV launch (engine.hip), then -- on more than one rank -- one RCCL
+// all-gather of the new contribution vector x' (this replaces the reduceByKey shuffle at
+// :139) and one all-gather of the 32-word exact partial record (replaces the driver-side
+// reduce at :125), then a one-thread finalize that produces the next round's addthis.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "host_graph.h"
+#include "prmi355x.h"
+
+using prmi::DevGraph;
+using prmi::HostGraph;
+
+struct pr_ctx {
+  pr_opts opts{};
+  int device = -1;
+  bool has_device = false;
+  hipStream_t stream = nullptr;
+  std::vector<hipEvent_t> kev;   // spmv-kernel event pairs (first 64 rounds)
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  ncclComm_t comm = nullptr;
+  std::string err;
+  HostGraph hg;
+  bool have_graph = false;
+  enum { SRC_NONE, SRC_TEXT, SRC_EDGES, SRC_RMAT } source = SRC_NONE;
+  DevGraph dg;
+  int last_iters = -1;           // rounds behind the current ranks (-1: no run yet)
+  bool host_ranks_valid = false;
+  std::vector<double> h_ranks;
+  double ms_ingest = 0;
+};
+
+namespace {
+
+int fail(pr_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(c, x)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      return fail((c), e_ == hipErrorOutOfMemory ? PR_E_OOM : PR_E_HIP,                \
+                  std::string(#x) + ": " + hipGetErrorString(e_));                     \
+  } while (0)
+
+#define NCCLCHK(c, x)                                                                  \
+  do {                                                                                 \
+    ncclResult_t r_ = (x);                                                             \
+    if (r_ != ncclSuccess)                                                             \
+      return fail((c), PR_E_RCCL, std::string(#x) + ": " + ncclGetErrorString(r_));    \
+  } while (0)
+
+int need_device(pr_ctx* c) {
+  if (!c) return PR_E_ARG;
+  if (!c->has_device) return fail(c, PR_E_NODEV, "context has no device (PR_DEVICE_NONE)");
+  HIPCHK(c, hipSetDevice(c->device));
+  return PR_OK;
+}
+
+int need_graph(pr_ctx* c) {
+  if (!c->have_graph) return fail(c, PR_E_ARG, "no graph: call pr_ingest_* / pr_load_edges / pr_generate_rmat first");
+  return PR_OK;
+}
+
+int need_comm(pr_ctx* c) {
+  if (c->opts.n_ranks > 1 && !c->comm)
+    return fail(c, PR_E_ARG, "n_ranks > 1 requires pr_comm_init before building a graph");
+  return PR_OK;
+}
+
+int build_device(pr_ctx* c, const prmi::BuildInput& in) {
+  std::string e;
+  int rc = prmi::dev_build(&c->dg, in, c->stream, &e);
+  if (rc) return fail(c, rc, "device build: " + e);
+  c->last_iters = -1;
+  c->host_ranks_valid = false;
+  if (c->opts.flags & PR_F_VERBOSE)
+    fprintf(stderr, "[prmi355x] rank %d build %.1f ms: n=%u nnz=%llu rows=%u local_rows=%u local_nnz=%llu bins=%zu hubs=%zu blocks=%u\n",
+            c->opts.rank, c->dg.ms_build, c->dg.n, (unsigned long long)c->dg.nnz, c->dg.R,
+            c->dg.lrows, (unsigned long long)c->dg.lnnz, c->dg.bins.size(), c->dg.hubs.size(),
+            c->dg.total_blocks);
+  return PR_OK;
+}
+
+bool read_file(const char* path, std::string* out) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  long sz = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  out->resize(sz > 0 ? static_cast<size_t>(sz) : 0);
+  size_t got = sz > 0 ? fread(&(*out)[0], 1, out->size(), f) : 0;
+  fclose(f);
+  return got == out->size();
+}
+
+// Ranks of the last run, on the host, by original vertex id.  Collective (p > 1).
+int gather_ranks(pr_ctx* c) {
+  if (c->host_ranks_valid) return PR_OK;
+  if (c->last_iters < 0) return fail(c, PR_E_ARG, "no completed pr_run");
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = prmi::dev_scatter_ranks(&c->dg, c->last_iters, c->stream);
+  if (rc) return fail(c, rc, "scatter ranks");
+  if (c->opts.n_ranks > 1 && c->dg.n)
+    NCCLCHK(c, ncclAllReduce(c->dg.r_full, c->dg.r_full, c->dg.n, ncclFloat64, ncclSum, c->comm, c->stream));
+  c->h_ranks.resize(c->dg.n);
+  if (c->dg.n)
+    HIPCHK(c, hipMemcpyAsync(c->h_ranks.data(), c->dg.r_full, 8ull * c->dg.n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->host_ranks_valid = true;
+  return PR_OK;
+}
+
+uint64_t pair_count(const pr_ctx* c) {
+  if (c->source == pr_ctx::SRC_TEXT) return c->hg.n_pairs;
+  if (c->hg.mapw.empty()) return c->dg.n;
+  uint64_t s = 0;
+  for (uint32_t w : c->hg.mapw) s += w;
+  return s;
+}
+
+// pair i -> (vertex, title).  Generated / in-memory graphs: title "v<id>" ("v<id>#j" for
+// the j-th extra title of an id mapped several times).
+struct PairIndex {
+  std::vector<uint64_t> first;  // in-memory graphs with mapw: first pair of each vertex
+};
+
+void pair_at(const pr_ctx* c, const PairIndex& pi, uint64_t i, uint32_t* v, std::string* title) {
+  if (c->source == pr_ctx::SRC_TEXT) {
+    *v = c->hg.pair_id[i];
+    title->assign(c->hg.titles.data() + c->hg.pair_off[i], c->hg.pair_len[i]);
+    return;
+  }
+  if (c->hg.mapw.empty()) {
+    *v = static_cast<uint32_t>(i);
+    *title = "v" + std::to_string(i);
+    return;
+  }
+  auto it = std::upper_bound(pi.first.begin(), pi.first.end(), i);
+  const uint32_t vv = static_cast<uint32_t>(it - pi.first.begin() - 1);
+  *v = vv;
+  const uint64_t j = i - pi.first[vv];
+  *title = "v" + std::to_string(vv) + (j ? "#" + std::to_string(j) : "");
+}
+
+PairIndex make_pair_index(const pr_ctx* c) {
+  PairIndex pi;
+  if (c->source != pr_ctx::SRC_TEXT && !c->hg.mapw.empty()) {
+    pi.first.resize(c->hg.mapw.size() + 1);
+    pi.first[0] = 0;
+    for (size_t v = 0; v < c->hg.mapw.size(); ++v) pi.first[v + 1] = pi.first[v] + c->hg.mapw[v];
+  }
+  return pi;
+}
+
+// PageRank.java:167-189: ranks.join(mappings) -> (rank,(id,title)) -> sortByKey(false) ->
+// take(k).  Ties (unspecified order in Spark) broken by (title bytes, id).
+int topk_rows(pr_ctx* c, uint32_t k, std::vector<uint64_t>* pairs_out) {
+  int rc = gather_ranks(c);
+  if (rc) return rc;
+  const PairIndex pi = make_pair_index(c);
+  const uint64_t np = pair_count(c);
+  struct Row {
+    double r;
+    uint64_t pair;
+    uint32_t v;
+  };
+  std::vector<Row> rows;
+  rows.reserve(std::min<uint64_t>(np, 1u << 20));
+  for (uint64_t i = 0; i < np; ++i) {
+    uint32_t v;
+    if (c->source == pr_ctx::SRC_TEXT) v = c->hg.pair_id[i];
+    else if (c->hg.mapw.empty()) v = static_cast<uint32_t>(i);
+    else {
+      std::string t;
+      pair_at(c, pi, i, &v, &t);
+    }
+    const double r = c->h_ranks[v];
+    if (r > 0.0) rows.push_back({r, i, v});
+  }
+  std::vector<std::string> tcache;
+  auto title_of = [&](const Row& x) {
+    uint32_t v;
+    std::string t;
+    pair_at(c, pi, x.pair, &v, &t);
+    return t;
+  };
+  auto less = [&](const Row& a, const Row& b) {
+    if (a.r != b.r) return a.r > b.r;
+    const std::string ta = title_of(a), tb = title_of(b);
+    if (ta != tb) return ta < tb;
+    return a.v < b.v;
+  };
+  const size_t kk = std::min<size_t>(k, rows.size());
+  std::partial_sort(rows.begin(), rows.begin() + kk, rows.end(), less);
+  pairs_out->clear();
+  for (size_t i = 0; i < kk; ++i) pairs_out->push_back(rows[i].pair);
+  return PR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pr_version(void) {
+  static const char v[] = "0.1";
+  return v;
+}
+
+void pr_opts_default(pr_opts* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->device = PR_DEVICE_FROM_RANK;
+  o->n_ranks = 1;
+  o->rank = 0;
+  o->topk = 100;
+}
+
+int pr_create(pr_ctx** out, const pr_opts* opts) {
+  if (!out) return PR_E_ARG;
+  *out = nullptr;
+  pr_ctx* c = new (std::nothrow) pr_ctx();
+  if (!c) return PR_E_OOM;
+  if (opts) c->opts = *opts; else pr_opts_default(&c->opts);
+  if (c->opts.n_ranks < 1 || c->opts.rank < 0 || c->opts.rank >= c->opts.n_ranks) {
+    delete c;
+    return PR_E_ARG;
+  }
+  if (c->opts.topk == 0) c->opts.topk = 100;
+  c->dg.p = c->opts.n_ranks;
+  c->dg.rank = c->opts.rank;
+  if (c->opts.device != PR_DEVICE_NONE) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+      delete c;
+      return PR_E_HIP;
+    }
+    c->device = c->opts.device >= 0 ? c->opts.device : c->opts.rank % ndev;
+    if (c->device >= ndev || hipSetDevice(c->device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev_start) != hipSuccess || hipEventCreate(&c->ev_stop) != hipSuccess) {
+      delete c;
+      return PR_E_HIP;
+    }
+    c->has_device = true;
+  }
+  *out = c;
+  return PR_OK;
+}
+
+void pr_destroy(pr_ctx* c) {
+  if (!c) return;
+  if (c->has_device) {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    prmi::dev_free(&c->dg);
+    for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+const char* pr_last_error(const pr_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pr_comm_unique_id(uint8_t id_out[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  if (!id_out) return PR_E_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return PR_E_RCCL;
+  std::memcpy(id_out, &id, 128);
+  return PR_OK;
+}
+
+int pr_comm_init(pr_ctx* c, const uint8_t id[128]) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  if (!id) return fail(c, PR_E_ARG, "null id");
+  if (c->comm) return PR_OK;
+  if (c->opts.n_ranks == 1) return PR_OK;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  NCCLCHK(c, ncclCommInitRank(&c->comm, c->opts.n_ranks, uid, c->opts.rank));
+  return PR_OK;
+}
+
+int pr_ingest_buffers(pr_ctx* c, const char* arcs, size_t alen, const char* map, size_t mlen) {
+  if (!c || (!arcs && alen) || (!map && mlen)) return fail(c, PR_E_ARG, "bad buffers");
+  int rc = need_comm(c);
+  if (rc) return rc;
+  auto t0 = std::chrono::steady_clock::now();
+  c->hg = HostGraph();
+  c->have_graph = false;
+  prmi::ParseError pe;
+  if (!prmi::ingest_text(arcs ? arcs : "", alen, map ? map : "", mlen, &c->hg, &pe)) {
+    c->hg = HostGraph();
+    return fail(c, PR_E_PARSE,
+                std::string("java.lang.ArrayIndexOutOfBoundsException: 1 (") +
+                    (pe.in_mapping ? "mapping" : "arcs") + " line " + std::to_string(pe.line) +
+                    ": \"" + pe.text + "\")");
+  }
+  c->ms_ingest = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->source = pr_ctx::SRC_TEXT;
+  if (c->has_device) {
+    prmi::BuildInput in;
+    in.n = c->hg.n;
+    in.m = c->hg.m_raw;
+    in.n_tot = c->hg.n_tot;
+    in.h_src = c->hg.src.data();
+    in.h_dst = c->hg.dst.data();
+    in.h_mapw = c->hg.mapw.data();
+    rc = build_device(c, in);
+    if (rc) return rc;
+    // raw edge lists are no longer needed on the host
+    std::vector<uint32_t>().swap(c->hg.src);
+    std::vector<uint32_t>().swap(c->hg.dst);
+  }
+  c->have_graph = true;
+  return PR_OK;
+}
+
+int pr_ingest_files(pr_ctx* c, const char* arcs_path, const char* mapping_path) {
+  if (!c || !arcs_path || !mapping_path) return fail(c, PR_E_ARG, "null path");
+  std::string a, m;
+  if (!read_file(arcs_path, &a)) return fail(c, PR_E_IO, std::string("cannot read ") + arcs_path);
+  if (!read_file(mapping_path, &m)) return fail(c, PR_E_IO, std::string("cannot read ") + mapping_path);
+  return pr_ingest_buffers(c, a.data(), a.size(), m.data(), m.size());
+}
+
+int pr_load_edges(pr_ctx* c, const uint32_t* src, const uint32_t* dst, uint64_t m, uint32_t n,
+                  const uint32_t* mapw, uint64_t n_tot) {
+  if (!c || (m && (!src || !dst))) return fail(c, PR_E_ARG, "bad edge arrays");
+  int rc = need_comm(c);
+  if (rc) return rc;
+  for (uint64_t i = 0; i < m; ++i)
+    if (src[i] >= n || dst[i] >= n) return fail(c, PR_E_ARG, "edge endpoint >= n");
+  c->hg = HostGraph();
+  c->have_graph = false;
+  c->hg.n = n;
+  c->hg.m_raw = m;
+  if (mapw) {
+    c->hg.mapw.assign(mapw, mapw + n);
+    c->hg.n_tot = n_tot;
+  } else {
+    c->hg.n_tot = n_tot ? n_tot : n;
+  }
+  c->source = pr_ctx::SRC_EDGES;
+  if (c->has_device) {
+    prmi::BuildInput in;
+    in.n = n;
+    in.m = m;
+    in.n_tot = c->hg.n_tot;
+    in.h_src = src;
+    in.h_dst = dst;
+    in.h_mapw = mapw;
+    rc = build_device(c, in);
+    if (rc) return rc;
+  }
+  c->have_graph = true;
+  return PR_OK;
+}
+
+int pr_generate_rmat(pr_ctx* c, int32_t scale, int32_t edge_factor, uint64_t seed) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_comm(c);
+  if (rc) return rc;
+  if (scale < 1 || scale > 31 || edge_factor < 1) return fail(c, PR_E_ARG, "bad R-MAT size");
+  c->hg = HostGraph();
+  c->have_graph = false;
+  c->hg.n = 1u << scale;
+  c->hg.m_raw = static_cast<uint64_t>(edge_factor) << scale;
+  c->hg.n_tot = c->hg.n;
+  c->source = pr_ctx::SRC_RMAT;
+  prmi::BuildInput in;
+  in.n = c->hg.n;
+  in.m = c->hg.m_raw;
+  in.n_tot = c->hg.n_tot;
+  in.rmat = true;
+  in.scale = scale;
+  in.edge_factor = edge_factor;
+  in.seed = seed;
+  rc = build_device(c, in);
+  if (rc) return rc;
+  c->have_graph = true;
+  return PR_OK;
+}
+
+int pr_graph_get_info(pr_ctx* c, pr_graph_info* o) {
+  if (!c || !o) return PR_E_ARG;
+  int rc = need_graph(c);
+  if (rc) return rc;
+  std::memset(o, 0, sizeof(*o));
+  o->n_vertices = c->hg.n;
+  o->raw_edges = c->hg.m_raw;
+  o->n_tot = c->hg.n_tot;
+  o->n_pairs = pair_count(c);
+  o->ms_ingest = c->ms_ingest;
+  if (c->has_device) {
+    o->nnz = c->dg.nnz;
+    o->dangling_entries = c->dg.n_dang_entries;
+    o->n_sources = static_cast<uint64_t>(c->dg.nA) + c->dg.nC;
+    o->n_rows = c->dg.R;
+    o->local_rows = c->dg.lrows;
+    o->local_nnz = c->dg.lnnz;
+    o->ms_build = c->dg.ms_build;
+  }
+  return PR_OK;
+}
+
+int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  if (iterations < 0) return fail(c, PR_E_ARG, "iterations < 0");
+  DevGraph* g = &c->dg;
+  pr_stats s{};
+  s.nnz = g->nnz;
+  s.n_vertices = g->n;
+  s.bytes_per_iter = 4ull * g->nnz + 24ull * g->n + 8;
+  c->host_ranks_valid = false;
+  c->last_iters = -1;
+  if (iterations == 0) {  // the loop never runs: ranks = 1.0 on sources (PageRank.java:76-83)
+    c->last_iters = 0;
+    if (st) *st = s;
+    return PR_OK;
+  }
+  if (g->W0 == 0) {  // round 1 reduces an empty danglingMap (PageRank.java:125)
+    s.failed_iteration = 1;
+    if (st) *st = s;
+    return fail(c, PR_E_EMPTY_DANGLING, "java.lang.UnsupportedOperationException: empty collection (iteration 1)");
+  }
+  const bool tracked = tol > 0.0 || (c->opts.flags & PR_F_TRACK_RESIDUAL);
+  const int nk = std::min(iterations, 64);
+  while (static_cast<int>(c->kev.size()) < 2 * nk) {
+    hipEvent_t e;
+    HIPCHK(c, hipEventCreate(&e));
+    c->kev.push_back(e);
+  }
+  rc = prmi::dev_reset_state(g, c->stream);
+  if (rc) return fail(c, rc, "reset state");
+  HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+  int done = iterations;
+  prmi::IterState hs{};
+  for (int t = 1; t <= iterations; ++t) {
+    const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
+    hipEvent_t e0 = t <= nk ? c->kev[2 * (t - 1)] : nullptr;
+    hipEvent_t e1 = t <= nk ? c->kev[2 * (t - 1) + 1] : nullptr;
+    rc = prmi::dev_round_compute(g, t, mode, c->stream, e0, e1);
+    if (rc) return fail(c, rc, "round compute");
+    if (c->opts.n_ranks > 1) {
+      double* xf = prmi::dev_x_out(g, t);
+      NCCLCHK(c, ncclGroupStart());
+      NCCLCHK(c, ncclAllGather(xf + static_cast<uint64_t>(g->rank) * g->maxA, xf, g->maxA, ncclFloat64, c->comm, c->stream));
+      NCCLCHK(c, ncclAllGather(g->rec_local, g->rec_all, prmi::REC_WORDS, ncclUint64, c->comm, c->stream));
+      NCCLCHK(c, ncclGroupEnd());
+    }
+    rc = prmi::dev_round_finalize(g, t, tracked, c->stream);
+    if (rc) return fail(c, rc, "round finalize");
+    if (tol > 0.0) {
+      HIPCHK(c, hipMemcpyAsync(&hs, g->state, sizeof(hs), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (hs.resid <= tol) {
+        done = t;
+        break;
+      }
+    }
+  }
+  HIPCHK(c, hipEventRecord(c->ev_stop, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&hs, g->state, sizeof(hs), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  HIPCHK(c, hipEventElapsedTime(&ms, c->ev_start, c->ev_stop));
+  double kms = 0.0;
+  const int nmeas = std::min(done, nk);
+  for (int t = 0; t < nmeas; ++t) {
+    float k = 0.f;
+    if (g->total_blocks && hipEventElapsedTime(&k, c->kev[2 * t], c->kev[2 * t + 1]) == hipSuccess) kms += k;
+  }
+  s.iterations = done;
+  s.ms_total = ms;
+  s.ms_per_iter = ms / done;
+  s.ms_spmv_kernel = nmeas ? kms / nmeas : 0.0;
+  s.gteps = s.ms_per_iter > 0 ? static_cast<double>(g->nnz) / (s.ms_per_iter * 1e-3) / 1e9 : 0.0;
+  s.residual = tracked ? hs.resid : 0.0;
+  s.rank_sum = tracked ? hs.rank_sum : 0.0;
+  // the reduce of round err_iter saw an empty danglingMap: the reference dies there
+  if (hs.err_iter != 0 && hs.err_iter <= done) {
+    s.failed_iteration = hs.err_iter;
+    if (st) *st = s;
+    return fail(c, PR_E_EMPTY_DANGLING,
+                "java.lang.UnsupportedOperationException: empty collection (iteration " +
+                    std::to_string(hs.err_iter) + ")");
+  }
+  c->last_iters = done;
+  if (st) *st = s;
+  return PR_OK;
+}
+
+int pr_get_ranks(pr_ctx* c, double* out, uint64_t n) {
+  if (!c || !out) return PR_E_ARG;
+  int rc = gather_ranks(c);
+  if (rc) return rc;
+  if (n < c->h_ranks.size()) return fail(c, PR_E_ARG, "output buffer too small");
+  std::memcpy(out, c->h_ranks.data(), 8 * c->h_ranks.size());
+  return PR_OK;
+}
+
+int pr_topk(pr_ctx* c, uint32_t k, uint64_t* pair_out, uint32_t* id_out, double* rank_out,
+            uint32_t* count) {
+  if (!c) return PR_E_ARG;
+  std::vector<uint64_t> rows;
+  int rc = topk_rows(c, k, &rows);
+  if (rc) return rc;
+  const PairIndex pi = make_pair_index(c);
+  for (size_t i = 0; i < rows.size(); ++i) {
+    uint32_t v;
+    std::string t;
+    pair_at(c, pi, rows[i], &v, &t);
+    if (pair_out) pair_out[i] = rows[i];
+    if (id_out) id_out[i] = v;
+    if (rank_out) rank_out[i] = c->h_ranks[v];
+  }
+  if (count) *count = static_cast<uint32_t>(rows.size());
+  return PR_OK;
+}
+
+int pr_write_top_page(pr_ctx* c, const char* path) {
+  if (!c) return PR_E_ARG;
+  std::vector<uint64_t> rows;
+  int rc = topk_rows(c, c->opts.topk, &rows);
+  if (rc) return rc;
+  if (c->opts.rank != 0) return PR_OK;
+  const PairIndex pi = make_pair_index(c);
+  std::string out;
+  char num[64];
+  for (uint64_t i : rows) {
+    uint32_t v;
+    std::string t;
+    pair_at(c, pi, i, &v, &t);
+    prmi::java_double_to_string(c->h_ranks[v], num, sizeof(num));
+    out += t;
+    out += '\t';
+    out += num;
+    out += '\n';
+  }
+  FILE* f = fopen(path ? path : "./topPage", "wb");
+  if (!f) return fail(c, PR_E_IO, std::string("java.io.IOException: cannot open ") + (path ? path : "./topPage"));
+  const size_t w = fwrite(out.data(), 1, out.size(), f);
+  const int cl = fclose(f);
+  if (w != out.size() || cl != 0) return fail(c, PR_E_IO, "java.io.IOException: short write");
+  return PR_OK;
+}
+
+int pr_id_string(pr_ctx* c, uint32_t v, char* buf, size_t cap, size_t* len) {
+  if (!c) return PR_E_ARG;
+  int rc = need_graph(c);
+  if (rc) return rc;
+  if (v >= c->hg.n) return fail(c, PR_E_ARG, "vertex out of range");
+  std::string s;
+  if (c->source == pr_ctx::SRC_TEXT) {
+    size_t n;
+    const char* p = c->hg.ids.get(v, &n);
+    s.assign(p, n);
+  } else {
+    s = std::to_string(v);
+  }
+  if (len) *len = s.size();
+  if (buf && cap) std::memcpy(buf, s.data(), std::min(cap, s.size()));
+  return PR_OK;
+}
+
+int pr_pair(pr_ctx* c, uint64_t i, uint32_t* id, char* title, size_t cap, size_t* len) {
+  if (!c) return PR_E_ARG;
+  int rc = need_graph(c);
+  if (rc) return rc;
+  if (i >= pair_count(c)) return fail(c, PR_E_ARG, "pair out of range");
+  const PairIndex pi = make_pair_index(c);
+  uint32_t v;
+  std::string t;
+  pair_at(c, pi, i, &v, &t);
+  if (id) *id = v;
+  if (len) *len = t.size();
+  if (title && cap) std::memcpy(title, t.data(), std::min(cap, t.size()));
+  return PR_OK;
+}
+
+int pr_get_degrees(pr_ctx* c, uint32_t* outdeg, uint32_t* indeg, uint32_t* dang_w, uint64_t n) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  const uint64_t nv = c->dg.n;
+  if (n < nv) return fail(c, PR_E_ARG, "buffer too small");
+  if (nv) {
+    if (outdeg) HIPCHK(c, hipMemcpyAsync(outdeg, c->dg.outdeg, 4 * nv, hipMemcpyDeviceToHost, c->stream));
+    if (indeg) HIPCHK(c, hipMemcpyAsync(indeg, c->dg.indeg, 4 * nv, hipMemcpyDeviceToHost, c->stream));
+    if (dang_w) HIPCHK(c, hipMemcpyAsync(dang_w, c->dg.dang_w, 4 * nv, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PR_OK;
+}
+
+int pr_edge_digest(pr_ctx* c, uint64_t digest_out[2]) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  if (!digest_out) return PR_E_ARG;
+  digest_out[0] = c->dg.digest[0];
+  digest_out[1] = c->dg.digest[1];
+  return PR_OK;
+}
+
+int pr_export_csr(pr_ctx* c, uint64_t* row_ptr, uint32_t* col, uint32_t* outdeg, uint32_t* dang_w,
+                  uint64_t* n_out, uint64_t* nnz_out) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  if (c->opts.n_ranks != 1) return fail(c, PR_E_ARG, "pr_export_csr needs a single-rank context");
+  const DevGraph& g = c->dg;
+  if (n_out) *n_out = g.n;
+  if (nnz_out) *nnz_out = g.nnz;
+  if (!row_ptr && !col && !outdeg && !dang_w) return PR_OK;
+  const uint32_t n = g.n;
+  std::vector<uint32_t> perm(n), od(n), dw(n);
+  if (n) {
+    HIPCHK(c, hipMemcpyAsync(perm.data(), g.perm, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(od.data(), g.outdeg, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dw.data(), g.dang_w, 4ull * n, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (row_ptr) {
+    HIPCHK(c, hipMemcpyAsync(row_ptr, g.row_ptr, 8ull * (g.lrows + 1), hipMemcpyDeviceToHost, c->stream));
+  }
+  if (col && g.nnz) HIPCHK(c, hipMemcpyAsync(col, g.col, 4ull * g.nnz, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (row_ptr)
+    for (uint64_t k = g.lrows + 1ull; k <= n; ++k) row_ptr[k] = g.nnz;
+  if (col) {
+    // x positions -> internal ids (p = 1: A rows keep their index, C sits after maxA = nA)
+    for (uint64_t e = 0; e < g.nnz; ++e) {
+      const uint32_t x = col[e];
+      col[e] = x < g.nA ? x : x - g.nA + g.R;
+    }
+  }
+  for (uint32_t k = 0; k < n; ++k) {
+    if (outdeg) outdeg[k] = od[perm[k]];
+    if (dang_w) dang_w[k] = dw[perm[k]];
+  }
+  return PR_OK;
+}
+
+int pr_format_double(double v, char* buf, size_t cap) {
+  return prmi::java_double_to_string(v, buf, cap);
+}
+
+}  // extern "C"

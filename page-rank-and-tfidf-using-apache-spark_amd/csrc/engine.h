@@ -1,0 +1,141 @@
+// Device engine interface (implemented in engine.hip; driven by api.cpp).
+//
+// Layout in HBM (DESIGN.md "Data layout"):
+//   internal vertex order  k = 0..n-1, sorted by (class, in-degree desc, original id):
+//     class A [0,nA)        in>=1, out>=1   rows and columns
+//     class B [nA,R)        in>=1, out==0   rows only (dangling pages that get links)
+//     class C [R,R+nC)      in==0, out>=1   columns only (rank undefined after round 1)
+//     class D [R+nC,n)      in==0, out==0   neither
+//   rows k < R are dealt to ranks round-robin: rank j owns k = l*p + j (local row l)
+//   x (contribution vector, fp64) positions:  A-row k -> (k%p)*maxA + k/p,
+//                                             C-vertex k -> p*maxA + (k-R)
+//   per rank: row_ptr u64[lrows+1], col u32[lnnz] (x positions, rows' sources in internal
+//   order), meta u32[lrows] (out-degree for A rows, dangling weight for B rows).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace prmi {
+
+constexpr int SA_LIMBS = 10;       // exact accumulator: 10 x 32-bit chunks, unit 2^-96
+constexpr int SA_BASE_EXP = -96;
+constexpr int NSHARD = 256;        // atomic shards for the per-iteration partials
+constexpr int REC_WORDS = 32;      // record: [0,10) dangling mass, [10] dangling count,
+                                   //         [11,21) sum|dr|, [21,31) sum r
+constexpr int REC_DSUM = 0, REC_DCNT = 10, REC_RESID = 11, REC_RSUM = 21;
+constexpr int BLOCK = 256;
+
+enum : uint16_t { KIND_BLOCK = 7, KIND_HUB = 8 };  // kinds 0..6: 2^kind lanes per row
+
+struct Bin {
+  uint32_t block_begin;  // first block of this bin in the fused grid
+  uint32_t row_begin, row_end;
+  uint32_t seg_begin;    // hub bins: first segment
+  uint16_t kind, cls;    // cls 0 = class A rows, 1 = class B rows
+  uint32_t pad;
+};
+
+struct HubSeg {
+  uint64_t e_begin, e_end;
+};
+
+struct HubRow {
+  uint32_t row, part_begin, part_end, cls;
+};
+
+struct IterState {
+  double a;          // addthis for the next round (PageRank.java:135-138)
+  double resid;      // relative L1 residual of the last round (tracked mode)
+  double resid_abs;
+  double rank_sum;
+  uint64_t dcnt;     // defined dangling entries after the last round
+  int32_t err_iter;  // first round whose reduce (:125) would see an empty RDD, 0 = none
+  int32_t iter;
+};
+
+struct Tuning {
+  int epl = 4;          // target edges per lane for the grouped bins
+  uint32_t kb = 1024;   // in-degree above which one workgroup takes a row
+  uint32_t kh = 16384;  // in-degree above which a row is split into segments
+  uint32_t seg = 4096;  // edges per hub segment
+};
+
+struct DevGraph {
+  bool built = false;
+  int p = 1, rank = 0;
+  uint32_t n = 0;
+  uint64_t m_raw = 0, nnz = 0, n_tot = 0;
+  uint32_t nA = 0, nB = 0, nC = 0, nD = 0, R = 0;
+  uint32_t maxA = 0;
+  uint64_t X = 0;                 // x length
+  uint32_t lrows = 0, lA = 0;
+  uint64_t lnnz = 0;
+  uint64_t W0 = 0;                // sum of dangling weights (round-1 dangling mass)
+  uint64_t n_dang_entries = 0;
+  uint64_t digest[2] = {0, 0};
+  double ms_build = 0;
+  // device arrays
+  uint64_t* row_ptr = nullptr;
+  uint32_t* col = nullptr;
+  uint32_t* meta = nullptr;
+  uint32_t* perm = nullptr;       // internal -> original
+  uint32_t* outdeg = nullptr;     // by original id
+  uint32_t* indeg = nullptr;
+  uint32_t* dang_w = nullptr;
+  double* x_init = nullptr;
+  double* xbuf[2] = {nullptr, nullptr};
+  double* r_loc[2] = {nullptr, nullptr};
+  double* r_full = nullptr;       // [n] by original id (output staging)
+  uint64_t* shards = nullptr;     // [NSHARD][REC_WORDS]
+  uint64_t* rec_local = nullptr;  // [REC_WORDS]
+  uint64_t* rec_all = nullptr;    // [p][REC_WORDS]
+  IterState* state = nullptr;
+  // schedule
+  std::vector<Bin> bins;
+  Bin* d_bins = nullptr;
+  uint32_t total_blocks = 0;
+  std::vector<HubRow> hubs;
+  HubRow* d_hubs = nullptr;
+  HubSeg* d_segs = nullptr;
+  double* hub_part = nullptr;
+  uint32_t n_parts = 0;
+  Tuning tune;
+};
+
+struct BuildInput {
+  uint32_t n = 0;
+  uint64_t m = 0;
+  uint64_t n_tot = 0;
+  const uint32_t* h_src = nullptr;  // host raw edges (dense ids) unless rmat
+  const uint32_t* h_dst = nullptr;
+  const uint32_t* h_mapw = nullptr; // host; nullptr = every id mapped once
+  bool rmat = false;
+  int scale = 0;
+  int edge_factor = 0;
+  uint64_t seed = 0;
+};
+
+// Builds the per-rank CSR and all iteration buffers.  Returns 0 or a PR_E_* code.
+int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err);
+void dev_free(DevGraph* g);
+
+// One round t (1-based) of the loop PageRank.java:92-164 for this rank's rows, up to the
+// point where x' and the partial record are ready for the exchange.
+// mode: 0 = x' only, 1 = also write r', 2 = tracked (r', exact residual + rank sum).
+int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev0,
+                      hipEvent_t ev1);
+// After the exchange: combine p records -> next round's addthis / error / residual.
+int dev_round_finalize(DevGraph* g, int t, bool tracked, hipStream_t s);
+// Round-1 state (r^0 == 1): a = W0 / n_tot.
+int dev_reset_state(DevGraph* g, hipStream_t s);
+// x' slot of this rank for round t (send buffer of the all-gather) and the full buffer.
+double* dev_x_out(DevGraph* g, int t);
+// Scatter this rank's final ranks into r_full (by original id; zeros elsewhere).
+// iterations == 0 reproduces ranks = 1.0 on sources (PageRank.java:76-83).
+int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s);
+
+}  // namespace prmi
