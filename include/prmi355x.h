@@ -114,6 +114,13 @@ const char* pr_last_error(const pr_ctx* ctx);
 int pr_comm_unique_id(uint8_t id_out[128]);
 int pr_comm_init(pr_ctx* ctx, const uint8_t id[128]);
 
+/* Single-process rank group: n contexts created with n_ranks = n and rank = 0..n-1 (on one
+ * device or several) exchange x and the partial records by device copies instead of RCCL.
+ * Then call the ingest/generate function on every member, pr_run_group() for the rounds,
+ * and pr_get_ranks / pr_topk / pr_write_top_page on any member. */
+int pr_comm_init_local(pr_ctx** ctxs, int32_t n);
+int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_stats* stats);
+
 /* textFile(arcs)/textFile(mapping) + mapToPair(split) + distinct + groupByKey + cache +
  * subtractByKey + distinct().count() (PageRank.java:26-60), then the device CSR build. */
 int pr_ingest_files(pr_ctx* ctx, const char* arcs_path, const char* mapping_path);

@@ -40,6 +40,7 @@ struct pr_ctx {
   bool host_ranks_valid = false;
   std::vector<double> h_ranks;
   double ms_ingest = 0;
+  std::vector<pr_ctx*> group;    // single-process rank group (pr_comm_init_local)
 };
 
 namespace {
@@ -77,7 +78,7 @@ int need_graph(pr_ctx* c) {
 }
 
 int need_comm(pr_ctx* c) {
-  if (c->opts.n_ranks > 1 && !c->comm)
+  if (c->opts.n_ranks > 1 && !c->comm && c->group.empty())
     return fail(c, PR_E_ARG, "n_ranks > 1 requires pr_comm_init before building a graph");
   return PR_OK;
 }
@@ -114,6 +115,22 @@ int gather_ranks(pr_ctx* c) {
   if (c->last_iters < 0) return fail(c, PR_E_ARG, "no completed pr_run");
   int rc = need_device(c);
   if (rc) return rc;
+  if (!c->group.empty()) {  // sum every member's scattered rows (one nonzero per page)
+    c->h_ranks.assign(c->dg.n, 0.0);
+    std::vector<double> part(c->dg.n);
+    for (pr_ctx* m : c->group) {
+      HIPCHK(c, hipSetDevice(m->device));
+      rc = prmi::dev_scatter_ranks(&m->dg, c->last_iters, m->stream);
+      if (rc) return fail(c, rc, "scatter ranks");
+      if (m->dg.n)
+        HIPCHK(c, hipMemcpyAsync(part.data(), m->dg.r_full, 8ull * m->dg.n, hipMemcpyDeviceToHost, m->stream));
+      HIPCHK(c, hipStreamSynchronize(m->stream));
+      for (uint32_t v = 0; v < m->dg.n; ++v) c->h_ranks[v] += part[v];
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    c->host_ranks_valid = true;
+    return PR_OK;
+  }
   rc = prmi::dev_scatter_ranks(&c->dg, c->last_iters, c->stream);
   if (rc) return fail(c, rc, "scatter ranks");
   if (c->opts.n_ranks > 1 && c->dg.n)
@@ -301,6 +318,112 @@ int pr_comm_init(pr_ctx* c, const uint8_t id[128]) {
   return PR_OK;
 }
 
+int pr_comm_init_local(pr_ctx** ctxs, int32_t n) {
+  if (!ctxs || n < 1) return PR_E_ARG;
+  std::vector<pr_ctx*> g(ctxs, ctxs + n);
+  for (int i = 0; i < n; ++i) {
+    pr_ctx* c = ctxs[i];
+    if (!c || !c->has_device || c->opts.n_ranks != n || c->opts.rank != i || c->comm)
+      return c ? fail(c, PR_E_ARG, "local group: member i must have n_ranks = n, rank = i, a device, no RCCL comm") : PR_E_ARG;
+  }
+  for (int i = 0; i < n; ++i) ctxs[i]->group = g;
+  return PR_OK;
+}
+
+int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_stats* st) {
+  if (!ctxs || n < 1) return PR_E_ARG;
+  pr_ctx* c0 = ctxs[0];
+  for (int i = 0; i < n; ++i) {
+    pr_ctx* c = ctxs[i];
+    if (!c || static_cast<int>(c->group.size()) != n || c->group[i] != c) return fail(c0, PR_E_ARG, "not a local group");
+    int rc = need_graph(c);
+    if (rc) return rc;
+  }
+  if (iterations < 0) return fail(c0, PR_E_ARG, "iterations < 0");
+  pr_stats s{};
+  s.nnz = c0->dg.nnz;
+  s.n_vertices = c0->dg.n;
+  s.bytes_per_iter = 4ull * c0->dg.nnz + 24ull * c0->dg.n + 8;
+  for (int i = 0; i < n; ++i) {
+    ctxs[i]->host_ranks_valid = false;
+    ctxs[i]->last_iters = -1;
+  }
+  auto finish = [&](int done) {
+    for (int i = 0; i < n; ++i) ctxs[i]->last_iters = done;
+  };
+  if (iterations == 0) {
+    finish(0);
+    if (st) *st = s;
+    return PR_OK;
+  }
+  if (c0->dg.W0 == 0) {
+    s.failed_iteration = 1;
+    if (st) *st = s;
+    return fail(c0, PR_E_EMPTY_DANGLING, "java.lang.UnsupportedOperationException: empty collection (iteration 1)");
+  }
+  const bool tracked = tol > 0.0 || (c0->opts.flags & PR_F_TRACK_RESIDUAL);
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(c0, hipSetDevice(ctxs[i]->device));
+    int rc = prmi::dev_reset_state(&ctxs[i]->dg, ctxs[i]->stream);
+    if (rc) return fail(c0, rc, "reset state");
+  }
+  int done = iterations;
+  prmi::IterState hs{};
+  for (int t = 1; t <= iterations; ++t) {
+    const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
+    for (int i = 0; i < n; ++i) {
+      HIPCHK(c0, hipSetDevice(ctxs[i]->device));
+      int rc = prmi::dev_round_compute(&ctxs[i]->dg, t, mode, ctxs[i]->stream, nullptr, nullptr);
+      if (rc) return fail(c0, rc, "round compute");
+    }
+    for (int i = 0; i < n; ++i) HIPCHK(c0, hipStreamSynchronize(ctxs[i]->stream));
+    // the all-gathers, as copies: slot r of x' and record r to every member
+    for (int r = 0; r < n; ++r) {
+      DevGraph* src = &ctxs[r]->dg;
+      const uint64_t off = static_cast<uint64_t>(r) * src->maxA;
+      for (int q = 0; q < n; ++q) {
+        DevGraph* dst = &ctxs[q]->dg;
+        if (q != r && src->maxA)
+          HIPCHK(c0, hipMemcpyPeer(prmi::dev_x_out(dst, t) + off, ctxs[q]->device,
+                                   prmi::dev_x_out(src, t) + off, ctxs[r]->device, 8ull * src->maxA));
+        HIPCHK(c0, hipMemcpyPeer(dst->rec_all + static_cast<uint64_t>(r) * prmi::REC_WORDS, ctxs[q]->device,
+                                 src->rec_local, ctxs[r]->device, 8ull * prmi::REC_WORDS));
+      }
+    }
+    for (int i = 0; i < n; ++i) {
+      HIPCHK(c0, hipSetDevice(ctxs[i]->device));
+      int rc = prmi::dev_round_finalize(&ctxs[i]->dg, t, tracked, ctxs[i]->stream);
+      if (rc) return fail(c0, rc, "round finalize");
+    }
+    HIPCHK(c0, hipMemcpyAsync(&hs, c0->dg.state, sizeof(hs), hipMemcpyDeviceToHost, c0->stream));
+    HIPCHK(c0, hipStreamSynchronize(c0->stream));
+    if (tol > 0.0 && hs.resid <= tol) {
+      done = t;
+      break;
+    }
+  }
+  for (int i = 0; i < n; ++i) HIPCHK(c0, hipStreamSynchronize(ctxs[i]->stream));
+  HIPCHK(c0, hipSetDevice(c0->device));
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  s.iterations = done;
+  s.ms_total = ms;
+  s.ms_per_iter = ms / done;
+  s.gteps = static_cast<double>(c0->dg.nnz) / (s.ms_per_iter * 1e-3) / 1e9;
+  s.residual = tracked ? hs.resid : 0.0;
+  s.rank_sum = tracked ? hs.rank_sum : 0.0;
+  if (hs.err_iter != 0 && hs.err_iter <= done) {
+    s.failed_iteration = hs.err_iter;
+    if (st) *st = s;
+    return fail(c0, PR_E_EMPTY_DANGLING,
+                "java.lang.UnsupportedOperationException: empty collection (iteration " +
+                    std::to_string(hs.err_iter) + ")");
+  }
+  finish(done);
+  if (st) *st = s;
+  return PR_OK;
+}
+
 int pr_ingest_buffers(pr_ctx* c, const char* arcs, size_t alen, const char* map, size_t mlen) {
   if (!c || (!arcs && alen) || (!map && mlen)) return fail(c, PR_E_ARG, "bad buffers");
   int rc = need_comm(c);
@@ -431,6 +554,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   rc = need_graph(c);
   if (rc) return rc;
   if (iterations < 0) return fail(c, PR_E_ARG, "iterations < 0");
+  if (!c->group.empty()) return pr_run_group(c->group.data(), static_cast<int32_t>(c->group.size()), iterations, tol, st);
   DevGraph* g = &c->dg;
   pr_stats s{};
   s.nnz = g->nnz;

@@ -62,6 +62,7 @@ struct Tuning {
   uint32_t kb = 1024;   // in-degree above which one workgroup takes a row
   uint32_t kh = 16384;  // in-degree above which a row is split into segments
   uint32_t seg = 4096;  // edges per hub segment
+  int nt = 0;           // non-temporal loads for the streamed CSR arrays
 };
 
 struct DevGraph {

@@ -173,19 +173,27 @@ struct StepArgs {
   uint64_t* shards;
 };
 
+// Streamed (read-once) operands: non-temporal loads keep them from evicting the hot part
+// of x from the XCD's L2 (NT = 1).
+template <int NT, class T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 // Partial sum of x[col[e]] over e = beg + lane, beg + lane + S, ... < end, with four
 // independent gathers in flight per lane.  Fixed order: depends on (end-beg, S) only.
-template <int S>
+template <int S, int NT>
 __device__ __forceinline__ double strided_sum(const uint32_t* __restrict__ col,
                                               const double* __restrict__ x, uint64_t beg,
                                               uint64_t end, int lane) {
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   for (uint64_t e = beg + lane; e < end; e += 4ull * S) {
     const uint64_t e1 = e + S, e2 = e + 2ull * S, e3 = e + 3ull * S;
-    const uint32_t c0 = col[e];
-    const uint32_t c1 = e1 < end ? col[e1] : 0u;
-    const uint32_t c2 = e2 < end ? col[e2] : 0u;
-    const uint32_t c3 = e3 < end ? col[e3] : 0u;
+    const uint32_t c0 = ld_stream<NT>(col + e);
+    const uint32_t c1 = e1 < end ? ld_stream<NT>(col + e1) : 0u;
+    const uint32_t c2 = e2 < end ? ld_stream<NT>(col + e2) : 0u;
+    const uint32_t c3 = e3 < end ? ld_stream<NT>(col + e3) : 0u;
     const double v0 = x[c0];
     const double v1 = e1 < end ? x[c1] : 0.0;
     const double v2 = e2 < end ? x[c2] : 0.0;
@@ -258,7 +266,7 @@ __device__ __forceinline__ void row_epilogue(const StepArgs& A, double a, uint32
 }
 
 // G lanes per row (G <= 64): a workgroup takes 256/G consecutive rows of one bin.
-template <int G, int MODE>
+template <int G, int MODE, int NT>
 __device__ __forceinline__ void group_tile(const StepArgs& A, double a, const Bin& b,
                                            uint32_t blk, uint64_t (*lds)[REC_WORDS]) {
   constexpr uint32_t RPB = BLOCK / G;
@@ -266,13 +274,15 @@ __device__ __forceinline__ void group_tile(const StepArgs& A, double a, const Bi
   const int gl = threadIdx.x % G;
   const bool active = row < b.row_end;
   double s = 0.0;
-  if (active) s = strided_sum<G>(A.col, A.x_in, A.row_ptr[row], A.row_ptr[row + 1], gl);
+  if (active)
+    s = strided_sum<G, NT>(A.col, A.x_in, ld_stream<NT>(A.row_ptr + row),
+                           ld_stream<NT>(A.row_ptr + row + 1), gl);
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
   row_epilogue<MODE>(A, a, b.cls, row, s, active && gl == 0, lds);
 }
 
-template <int MODE>
+template <int MODE, int NT>
 __global__ __launch_bounds__(BLOCK) void spmv_round(StepArgs A) {
   __shared__ uint64_t lds[4][REC_WORDS];
   __shared__ double red[4];
@@ -286,17 +296,17 @@ __global__ __launch_bounds__(BLOCK) void spmv_round(StepArgs A) {
   const uint32_t blk = b - bin.block_begin;
   const double a = A.st->a;
   switch (bin.kind) {
-    case 0: group_tile<1, MODE>(A, a, bin, blk, lds); break;
-    case 1: group_tile<2, MODE>(A, a, bin, blk, lds); break;
-    case 2: group_tile<4, MODE>(A, a, bin, blk, lds); break;
-    case 3: group_tile<8, MODE>(A, a, bin, blk, lds); break;
-    case 4: group_tile<16, MODE>(A, a, bin, blk, lds); break;
-    case 5: group_tile<32, MODE>(A, a, bin, blk, lds); break;
-    case 6: group_tile<64, MODE>(A, a, bin, blk, lds); break;
+    case 0: group_tile<1, MODE, NT>(A, a, bin, blk, lds); break;
+    case 1: group_tile<2, MODE, NT>(A, a, bin, blk, lds); break;
+    case 2: group_tile<4, MODE, NT>(A, a, bin, blk, lds); break;
+    case 3: group_tile<8, MODE, NT>(A, a, bin, blk, lds); break;
+    case 4: group_tile<16, MODE, NT>(A, a, bin, blk, lds); break;
+    case 5: group_tile<32, MODE, NT>(A, a, bin, blk, lds); break;
+    case 6: group_tile<64, MODE, NT>(A, a, bin, blk, lds); break;
     case KIND_BLOCK: {
       const uint32_t row = bin.row_begin + blk;
-      double s = strided_sum<BLOCK>(A.col, A.x_in, A.row_ptr[row], A.row_ptr[row + 1],
-                                    threadIdx.x);
+      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, A.row_ptr[row], A.row_ptr[row + 1],
+                                        threadIdx.x);
       s = block_sum(s, red);
       row_epilogue<MODE>(A, a, bin.cls, row, s, threadIdx.x == 0, lds);
       break;
@@ -304,7 +314,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_round(StepArgs A) {
     default: {  // KIND_HUB: one segment of a split row -> partial (combined in hub_round)
       const uint32_t sg = bin.seg_begin + blk;
       const HubSeg seg = A.segs[sg];
-      double s = strided_sum<BLOCK>(A.col, A.x_in, seg.e_begin, seg.e_end, threadIdx.x);
+      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, seg.e_begin, seg.e_end, threadIdx.x);
       s = block_sum(s, red);
       if (threadIdx.x == 0) A.hub_part[sg] = s;
       break;
@@ -638,6 +648,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   g->tune.kb = static_cast<uint32_t>(std::max(64, env_int("PR_KB", static_cast<int>(g->tune.kb))));
   g->tune.kh = static_cast<uint32_t>(std::max(static_cast<int>(g->tune.kb), env_int("PR_KH", static_cast<int>(g->tune.kh))));
   g->tune.seg = static_cast<uint32_t>(std::max(256, env_int("PR_SEG", static_cast<int>(g->tune.seg))));
+  g->tune.nt = env_int("PR_NT", g->tune.nt);
   const uint32_t n = in.n;
   const uint64_t m = in.m;
   g->n = n;
@@ -943,9 +954,16 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.shards = g->shards;
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
   if (g->total_blocks) {
-    if (mode == 0) hipLaunchKernelGGL(spmv_round<0>, dim3(g->total_blocks), dim3(BLOCK), 0, s, A);
-    else if (mode == 1) hipLaunchKernelGGL(spmv_round<1>, dim3(g->total_blocks), dim3(BLOCK), 0, s, A);
-    else hipLaunchKernelGGL(spmv_round<2>, dim3(g->total_blocks), dim3(BLOCK), 0, s, A);
+    const dim3 gr(g->total_blocks), bl(BLOCK);
+    if (g->tune.nt) {
+      if (mode == 0) hipLaunchKernelGGL((spmv_round<0, 1>), gr, bl, 0, s, A);
+      else if (mode == 1) hipLaunchKernelGGL((spmv_round<1, 1>), gr, bl, 0, s, A);
+      else hipLaunchKernelGGL((spmv_round<2, 1>), gr, bl, 0, s, A);
+    } else {
+      if (mode == 0) hipLaunchKernelGGL((spmv_round<0, 0>), gr, bl, 0, s, A);
+      else if (mode == 1) hipLaunchKernelGGL((spmv_round<1, 0>), gr, bl, 0, s, A);
+      else hipLaunchKernelGGL((spmv_round<2, 0>), gr, bl, 0, s, A);
+    }
   }
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
   if (!g->hubs.empty()) {

@@ -128,6 +128,8 @@ def lib():
         "pr_last_error": (C.c_char_p, [P]),
         "pr_comm_unique_id": (I32, [C.c_char_p]),
         "pr_comm_init": (I32, [P, C.c_char_p]),
+        "pr_comm_init_local": (I32, [C.POINTER(P), I32]),
+        "pr_run_group": (I32, [C.POINTER(P), I32, I32, D, C.POINTER(Stats)]),
         "pr_ingest_files": (I32, [P, C.c_char_p, C.c_char_p]),
         "pr_ingest_buffers": (I32, [P, C.c_char_p, SZ, C.c_char_p, SZ]),
         "pr_load_edges": (I32, [P, P, P, U64, U32, P, U64]),
@@ -292,6 +294,32 @@ class Engine:
         self._check(lib().pr_export_csr(self._h, _ptr(rp), _ptr(col), _ptr(od), _ptr(dw),
                                         C.byref(n), C.byref(nnz)))
         return rp, col[:nnz.value], od[:n.value], dw[:n.value]
+
+
+class LocalGroup:
+    """n engine contexts in this process acting as ranks 0..n-1 (device copies replace RCCL)."""
+
+    def __init__(self, n: int, devices: Optional[Sequence[int]] = None, flags: int = 0):
+        devs = list(devices) if devices is not None else [0] * n
+        self.members = [Engine(device=devs[i], n_ranks=n, rank=i, flags=flags) for i in range(n)]
+        self._arr = (C.c_void_p * n)(*[m._h for m in self.members])
+        rc = lib().pr_comm_init_local(self._arr, n)
+        if rc:
+            raise PageRankError(rc, "pr_comm_init_local failed")
+
+    def each(self, fn, *args):
+        for m in self.members:
+            getattr(m, fn)(*args)
+
+    def run(self, iterations: int = 10, tol: float = 0.0) -> Dict[str, float]:
+        st = Stats()
+        rc = lib().pr_run_group(self._arr, len(self.members), iterations, tol, C.byref(st))
+        self.members[0]._check(rc)
+        return st.as_dict()
+
+    def close(self):
+        for m in self.members:
+            m.close()
 
 
 class PageRank:

@@ -241,3 +241,38 @@ def test_pagerank_main_cli_contract(P, O, tmp_path):
     subprocess.run([cli, str(tmp_path / "a"), str(tmp_path / "m"), "10", "--out", str(out2)],
                    check=True, timeout=120)
     assert out2.read_bytes() == out.read_bytes()
+
+
+# ---- multi-rank layout on one GPU: single-process rank group (copies replace RCCL) -------
+@pytest.mark.parametrize("p", [2, 3, 4, 8])
+def test_rank_group_bit_identical_to_single(P, p):
+    ref = P.Engine()
+    ref.generate_rmat(15, 16, 6)
+    ref.run(10)
+    r1 = ref.ranks()
+    grp = P.LocalGroup(p)
+    grp.each("generate_rmat", 15, 16, 6)
+    info = [m.info() for m in grp.members]
+    assert sum(i["local_nnz"] for i in info) == info[0]["nnz"]
+    assert sum(i["local_rows"] for i in info) == info[0]["n_rows"]
+    grp.run(10)
+    rp = grp.members[p - 1].ranks()
+    assert np.array_equal(r1.view(np.uint64), rp.view(np.uint64))
+    assert grp.members[0].topk(100) == ref.topk(100)
+    grp.close()
+
+
+def test_rank_group_text_and_errors(P, O):
+    arcs, mapping = G.wiki_text(seed=5, pages=3000, arcs_target=30000)
+    g = O.Graph.from_text(arcs, mapping)
+    grp = P.LocalGroup(3)
+    grp.each("ingest_buffers", arcs, mapping)
+    grp.run(10)
+    parity.assert_ranks_close(grp.members[1].ranks(), g.run(10)["ranks"])
+    st = grp.run(100, 1e-10)                       # tracked residual across ranks
+    res = g.run(100, tol=1e-10)
+    assert abs(st["iterations"] - res["iterations"]) <= 1
+    bad = P.LocalGroup(2)
+    bad.each("ingest_buffers", b"1\t2\n1\t3\n2\t3\n3\t1\n4\t3\n", b"1\tA\n2\tB\n3\tC\n4\tD\n5\tE\n")
+    with pytest.raises(P.UnsupportedOperationException, match="iteration 2"):
+        bad.run(5)
