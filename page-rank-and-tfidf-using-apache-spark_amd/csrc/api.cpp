@@ -378,17 +378,20 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       if (rc) return fail(c0, rc, "round compute");
     }
     for (int i = 0; i < n; ++i) HIPCHK(c0, hipStreamSynchronize(ctxs[i]->stream));
-    // the all-gathers, as copies: slot r of x' and record r to every member
-    for (int r = 0; r < n; ++r) {
-      DevGraph* src = &ctxs[r]->dg;
-      const uint64_t off = static_cast<uint64_t>(r) * src->maxA;
-      for (int q = 0; q < n; ++q) {
-        DevGraph* dst = &ctxs[q]->dg;
+    // the all-gathers, as copies on each receiver's stream: slot r of x', record r
+    for (int q = 0; q < n; ++q) {
+      DevGraph* dst = &ctxs[q]->dg;
+      HIPCHK(c0, hipSetDevice(ctxs[q]->device));
+      for (int r = 0; r < n; ++r) {
+        DevGraph* src = &ctxs[r]->dg;
+        const uint64_t off = static_cast<uint64_t>(r) * src->maxA;
         if (q != r && src->maxA)
-          HIPCHK(c0, hipMemcpyPeer(prmi::dev_x_out(dst, t) + off, ctxs[q]->device,
-                                   prmi::dev_x_out(src, t) + off, ctxs[r]->device, 8ull * src->maxA));
-        HIPCHK(c0, hipMemcpyPeer(dst->rec_all + static_cast<uint64_t>(r) * prmi::REC_WORDS, ctxs[q]->device,
-                                 src->rec_local, ctxs[r]->device, 8ull * prmi::REC_WORDS));
+          HIPCHK(c0, hipMemcpyPeerAsync(prmi::dev_x_out(dst, t) + off, ctxs[q]->device,
+                                        prmi::dev_x_out(src, t) + off, ctxs[r]->device,
+                                        8ull * src->maxA, ctxs[q]->stream));
+        HIPCHK(c0, hipMemcpyPeerAsync(dst->rec_all + static_cast<uint64_t>(r) * prmi::REC_WORDS,
+                                      ctxs[q]->device, src->rec_local, ctxs[r]->device,
+                                      8ull * prmi::REC_WORDS, ctxs[q]->stream));
       }
     }
     for (int i = 0; i < n; ++i) {
@@ -396,6 +399,7 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       int rc = prmi::dev_round_finalize(&ctxs[i]->dg, t, tracked, ctxs[i]->stream);
       if (rc) return fail(c0, rc, "round finalize");
     }
+    for (int i = 0; i < n; ++i) HIPCHK(c0, hipStreamSynchronize(ctxs[i]->stream));
     HIPCHK(c0, hipMemcpyAsync(&hs, c0->dg.state, sizeof(hs), hipMemcpyDeviceToHost, c0->stream));
     HIPCHK(c0, hipStreamSynchronize(c0->stream));
     if (tol > 0.0 && hs.resid <= tol) {
@@ -636,6 +640,19 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   }
   c->last_iters = done;
   if (st) *st = s;
+  if (!g->split_ms.empty()) {  // PR_SPLIT timing breakdown (per bin, summed over rounds)
+    const size_t nsb = g->sbins.size();
+    for (size_t i = 0; i < g->split_ms.size(); ++i) {
+      const bool sl = i < nsb;
+      const prmi::Bin& b = sl ? g->sbins[i] : g->bins[i - nsb];
+      const uint64_t edges = sl ? g->sbin_edges[i] : g->bin_edges[i - nsb];
+      const double ms = g->split_ms[i] / done;
+      fprintf(stderr, "[prmi355x] %s bin %2zu kind %u cls %u rows %9u edges %11llu  %8.3f ms/round  %6.1f GTEPS\n",
+              sl ? "slice" : "row  ", sl ? i : i - nsb, b.kind, b.cls, b.row_end - b.row_begin,
+              (unsigned long long)edges, ms, ms > 0 ? edges / (ms * 1e6) : 0.0);
+    }
+    std::fill(g->split_ms.begin(), g->split_ms.end(), 0.0);
+  }
   return PR_OK;
 }
 
@@ -780,10 +797,19 @@ int pr_export_csr(pr_ctx* c, uint64_t* row_ptr, uint32_t* col, uint32_t* outdeg,
   if (row_ptr)
     for (uint64_t k = g.lrows + 1ull; k <= n; ++k) row_ptr[k] = g.nnz;
   if (col) {
-    // x positions -> internal ids (p = 1: A rows keep their index, C sits after maxA = nA)
+    // x positions -> internal ids (p = 1; inverse of the device layout)
+    const uint32_t CH = prmi::CHUNK, NS = prmi::NSLICE;
     for (uint64_t e = 0; e < g.nnz; ++e) {
-      const uint32_t x = col[e];
-      col[e] = x < g.nA ? x : x - g.nA + g.R;
+      const uint32_t x = col[e] & 0x7FFFFFFFu;  // bit 31: cold-gather marker
+      if (!g.sm) {
+        col[e] = x < g.maxA ? x : x - g.maxA + g.R;
+      } else if (x < g.maxA) {
+        const uint32_t sl = x / g.SL, r = x % g.SL;
+        col[e] = ((r / CH) * NS + sl) * CH + r % CH;
+      } else {
+        const uint32_t q = x - g.maxA, sl = q / g.SLC, r = q % g.SLC;
+        col[e] = g.R + ((r / CH) * NS + sl) * CH + r % CH;
+      }
     }
   }
   for (uint32_t k = 0; k < n; ++k) {

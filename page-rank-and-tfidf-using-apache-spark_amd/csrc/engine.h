@@ -6,11 +6,12 @@
 //     class B [nA,R)        in>=1, out==0   rows only (dangling pages that get links)
 //     class C [R,R+nC)      in==0, out>=1   columns only (rank undefined after round 1)
 //     class D [R+nC,n)      in==0, out==0   neither
-//   rows k < R are dealt to ranks round-robin: rank j owns k = l*p + j (local row l)
-//   x (contribution vector, fp64) positions:  A-row k -> (k%p)*maxA + k/p,
-//                                             C-vertex k -> p*maxA + (k-R)
-//   per rank: row_ptr u64[lrows+1], col u32[lnnz] (x positions, rows' sources in internal
-//   order), meta u32[lrows] (out-degree for A rows, dangling weight for B rows).
+//   rows k < R are dealt to ranks in chunks of 16: chunk c = k>>4 goes to rank c % p
+//   XCD slicing: the columns of x are cut into 8 slices by 128-byte chunk (slice = chunk
+//   index mod 8); the edges of a row with in-degree >= ks are grouped by slice, and slice
+//   j's partial sums are computed only by workgroups with blockIdx % 8 == j (one XCD), so
+//   each XCD's L2 caches 1/8 of x.  x is stored slice-major (p divides 8): rank slot, then
+//   slice region, then chunks in hotness order -- each slice is one contiguous range.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,19 +29,24 @@ constexpr int REC_WORDS = 32;      // record: [0,10) dangling mass, [10] danglin
                                    //         [11,21) sum|dr|, [21,31) sum r
 constexpr int REC_DSUM = 0, REC_DCNT = 10, REC_RESID = 11, REC_RSUM = 21;
 constexpr int BLOCK = 256;
+constexpr int NSLICE = 8;          // one slice per XCD
+constexpr int CHUNK = 16;          // rows dealt per rank chunk = entries per 128-B x line
 
-enum : uint16_t { KIND_BLOCK = 7, KIND_HUB = 8 };  // kinds 0..6: 2^kind lanes per row
+// kinds 0..6: 2^kind lanes per row; then one workgroup per row; hub segment; combine
+enum : uint16_t { KIND_BLOCK = 7, KIND_HUB = 8, KIND_COMBINE = 9 };
 
 struct Bin {
-  uint32_t block_begin;  // first block of this bin in the fused grid
+  uint32_t block_begin;  // first tile of this bin in its launch's grid
   uint32_t row_begin, row_end;
-  uint32_t seg_begin;    // hub bins: first segment
+  uint32_t seg_begin;    // hub bins: first segment (tile) index
   uint16_t kind, cls;    // cls 0 = class A rows, 1 = class B rows
-  uint32_t pad;
+  uint32_t srow_begin;   // sliced rows: slice-row index of row_begin
 };
 
 struct HubSeg {
   uint64_t e_begin, e_end;
+  uint32_t part;         // hub_part slot (UINT32_MAX: padding, nothing to write)
+  uint32_t pad;
 };
 
 struct HubRow {
@@ -59,10 +65,15 @@ struct IterState {
 
 struct Tuning {
   int epl = 4;          // target edges per lane for the grouped bins
-  uint32_t kb = 1024;   // in-degree above which one workgroup takes a row
+  uint32_t kb = 1024;   // (sub-)row length above which one workgroup takes a row
   uint32_t kh = 16384;  // in-degree above which a row is split into segments
   uint32_t seg = 4096;  // edges per hub segment
+  uint32_t ks = 64;     // in-degree from which a row is XCD-sliced (PR_KS; huge = off)
   int nt = 0;           // non-temporal loads for the streamed CSR arrays
+  uint32_t hot = 0x7FFFFFFFu;  // PR_HOT: entries per slice region gathered with normal
+                               // loads; columns beyond are gathered non-temporally
+  uint32_t colmask = 0xFFFFFFFFu;  // PR_COLMASK: timing-only gather working-set restriction
+  int split = 0;        // PR_SPLIT: one launch per bin with events (timing breakdown only)
 };
 
 struct DevGraph {
@@ -71,7 +82,9 @@ struct DevGraph {
   uint32_t n = 0;
   uint64_t m_raw = 0, nnz = 0, n_tot = 0;
   uint32_t nA = 0, nB = 0, nC = 0, nD = 0, R = 0;
-  uint32_t maxA = 0;
+  uint32_t maxA = 0;              // x slot length per rank
+  bool sm = false;                // slice-major x layout (p divides 8)
+  uint32_t SL = 0, SLC = 0;       // slice region lengths (class A / class C)
   uint64_t X = 0;                 // x length
   uint32_t lrows = 0, lA = 0;
   uint64_t lnnz = 0;
@@ -79,6 +92,8 @@ struct DevGraph {
   uint64_t n_dang_entries = 0;
   uint64_t digest[2] = {0, 0};
   double ms_build = 0;
+  // sliced rows: class A [0,sA), class B [lA,lA+sB); hubs lead each range (hA, hB)
+  uint32_t sA = 0, sB = 0, hA = 0, hB = 0, nS = 0;
   // device arrays
   uint64_t* row_ptr = nullptr;
   uint32_t* col = nullptr;
@@ -87,6 +102,8 @@ struct DevGraph {
   uint32_t* outdeg = nullptr;     // by original id
   uint32_t* indeg = nullptr;
   uint32_t* dang_w = nullptr;
+  uint32_t* sb = nullptr;         // [9][nS] slice offsets inside each sliced row
+  double* part = nullptr;         // [8][nS] per-slice partial row sums
   double* x_init = nullptr;
   double* xbuf[2] = {nullptr, nullptr};
   double* r_loc[2] = {nullptr, nullptr};
@@ -95,16 +112,26 @@ struct DevGraph {
   uint64_t* rec_local = nullptr;  // [REC_WORDS]
   uint64_t* rec_all = nullptr;    // [p][REC_WORDS]
   IterState* state = nullptr;
-  // schedule
+  // schedule: the row launch (light rows + combine + unsliced hubs) ...
   std::vector<Bin> bins;
+  std::vector<uint64_t> bin_edges;
   Bin* d_bins = nullptr;
   uint32_t total_blocks = 0;
+  HubSeg* d_segs = nullptr;       // unsliced hub segments
+  // ... and the slice launch (grid = 8 x slice_tiles)
+  std::vector<Bin> sbins;
+  std::vector<uint64_t> sbin_edges;
+  Bin* d_sbins = nullptr;
+  uint32_t slice_tiles = 0;
+  HubSeg* d_ssegs = nullptr;      // [8][hub tiles] sliced hub segments (padded)
+  uint32_t hub_tiles = 0;
   std::vector<HubRow> hubs;
   HubRow* d_hubs = nullptr;
-  HubSeg* d_segs = nullptr;
   double* hub_part = nullptr;
   uint32_t n_parts = 0;
   Tuning tune;
+  std::vector<hipEvent_t> split_ev;  // PR_SPLIT timing mode
+  std::vector<double> split_ms;
 };
 
 struct BuildInput {
@@ -133,10 +160,15 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
 int dev_round_finalize(DevGraph* g, int t, bool tracked, hipStream_t s);
 // Round-1 state (r^0 == 1): a = W0 / n_tot.
 int dev_reset_state(DevGraph* g, hipStream_t s);
-// x' slot of this rank for round t (send buffer of the all-gather) and the full buffer.
+// x' buffer of round t (this rank's slot starts at rank*maxA).
 double* dev_x_out(DevGraph* g, int t);
 // Scatter this rank's final ranks into r_full (by original id; zeros elsewhere).
 // iterations == 0 reproduces ranks = 1.0 on sources (PageRank.java:76-83).
 int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s);
+// Internal id of this rank's local row l (host copy of the device mapping).
+inline uint32_t row_internal(const DevGraph* g, uint32_t l) {
+  return (((l / CHUNK) * static_cast<uint32_t>(g->p) + static_cast<uint32_t>(g->rank)) * CHUNK) +
+         (l % CHUNK);
+}
 
 }  // namespace prmi

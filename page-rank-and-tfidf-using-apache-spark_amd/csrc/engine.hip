@@ -2,8 +2,9 @@
 //
 // Replaces, per round, PageRank.java:94-160 -- the contribution flatMapToPair (:94-117), the
 // dangling-mass reduce (:121-138), reduceByKey(Sum) (:139, Sum :208-213) and the damping /
-// dangling-update maps (:140-160) -- with ONE fused pull-SpMV launch over the transposed
-// graph plus two single-workgroup reductions.  The graph build (K1) replaces
+// dangling-update maps (:140-160) -- with a pull SpMV over the transposed graph in two
+// launches (XCD-sliced partial sums for heavy rows; a fused row launch that combines them,
+// handles the light rows and applies the epilogue) plus two single-workgroup reductions.  The graph build (K1) replaces
 // distinct().groupByKey() (:42), the urlCount loop (:103-108) and subtractByKey (:56).
 //
 // Numerics (DESIGN.md "Parity"):
@@ -154,7 +155,7 @@ __device__ double sa_to_double_dev(const uint64_t* limb) {
 }
 
 // =======================================================================================
-// the fused round: pull SpMV + damping epilogue + exact partials
+// the round: XCD-sliced partial sums + fused row launch (combine / light rows / epilogue)
 // =======================================================================================
 struct StepArgs {
   const Bin* bins;
@@ -166,12 +167,35 @@ struct StepArgs {
   double* x_out;          // this rank's slot of the next x
   const double* r_old;    // tracked mode: previous ranks (nullptr = r^0 == 1)
   double* r_out;
-  const HubSeg* segs;
+  const HubSeg* segs;     // hub segments of this launch
   double* hub_part;
   const HubRow* hubs;
   const IterState* st;
   uint64_t* shards;
+  const uint32_t* sb;     // [9][nS] slice offsets of sliced rows
+  double* part;           // [8][nS] slice partials
+  uint32_t nS;
+  uint32_t hub_tiles;     // per-slice stride of the sliced hub segment table
+  uint32_t colmask;       // timing experiments only (PR_COLMASK); all-ones in production
+  uint32_t block_base;    // first grid block of this launch (PR_SPLIT timing mode)
+  uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
 };
+
+// offset of local row l's x entry inside this rank's slot (see Layout / xpos)
+__device__ __forceinline__ uint32_t xslot_of(const StepArgs& A, uint32_t l) {
+  if (!A.sm) return l;
+  const uint32_t c = (l / CHUNK) * A.p + A.rank, sl = c % NSLICE;
+  return (sl / A.p) * A.SL + (c / NSLICE) * CHUNK + (l % CHUNK);
+}
+
+__device__ __forceinline__ int find_bin(const Bin* bins, int nbins, uint32_t t) {
+  int lo = 0, hi = nbins - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (bins[mid].block_begin <= t) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
 
 // Streamed (read-once) operands: non-temporal loads keep them from evicting the hot part
 // of x from the XCD's L2 (NT = 1).
@@ -183,10 +207,20 @@ __device__ __forceinline__ T ld_stream(const T* p) {
 
 // Partial sum of x[col[e]] over e = beg + lane, beg + lane + S, ... < end, with four
 // independent gathers in flight per lane.  Fixed order: depends on (end-beg, S) only.
+// Gather of x[c]; bit 31 of a column index marks a cold entry (beyond the L2-resident
+// prefix of its slice): it is loaded non-temporally so it does not evict hot lines.
+template <int NT>
+__device__ __forceinline__ double gather_x(const double* __restrict__ x, uint32_t raw,
+                                           uint32_t cm) {
+  const uint32_t c = raw & 0x7FFFFFFFu & cm;
+  if (raw >> 31) return __builtin_nontemporal_load(x + c);
+  return x[c];
+}
+
 template <int S, int NT>
 __device__ __forceinline__ double strided_sum(const uint32_t* __restrict__ col,
                                               const double* __restrict__ x, uint64_t beg,
-                                              uint64_t end, int lane) {
+                                              uint64_t end, int lane, uint32_t cm) {
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   for (uint64_t e = beg + lane; e < end; e += 4ull * S) {
     const uint64_t e1 = e + S, e2 = e + 2ull * S, e3 = e + 3ull * S;
@@ -194,10 +228,10 @@ __device__ __forceinline__ double strided_sum(const uint32_t* __restrict__ col,
     const uint32_t c1 = e1 < end ? ld_stream<NT>(col + e1) : 0u;
     const uint32_t c2 = e2 < end ? ld_stream<NT>(col + e2) : 0u;
     const uint32_t c3 = e3 < end ? ld_stream<NT>(col + e3) : 0u;
-    const double v0 = x[c0];
-    const double v1 = e1 < end ? x[c1] : 0.0;
-    const double v2 = e2 < end ? x[c2] : 0.0;
-    const double v3 = e3 < end ? x[c3] : 0.0;
+    const double v0 = gather_x<NT>(x, c0, cm);
+    const double v1 = e1 < end ? gather_x<NT>(x, c1, cm) : 0.0;
+    const double v2 = e2 < end ? gather_x<NT>(x, c2, cm) : 0.0;
+    const double v3 = e3 < end ? gather_x<NT>(x, c3, cm) : 0.0;
     s0 += v0;
     s1 += v1;
     s2 += v2;
@@ -228,7 +262,7 @@ __device__ __forceinline__ void row_epilogue(const StepArgs& A, double a, uint32
     r = c > 0.0 ? __dadd_rn(0.15, __dmul_rn(__dadd_rn(c, a), 0.85)) : 0.0;
     const uint32_t mt = A.meta[row];
     if (cls == 0)
-      A.x_out[row] = r / static_cast<double>(mt);  // :113  rank / urlCount
+      A.x_out[xslot_of(A, row)] = r / static_cast<double>(mt);  // :113  rank / urlCount
     else
       w = mt;
     if (MODE >= 1) A.r_out[row] = r;
@@ -276,23 +310,35 @@ __device__ __forceinline__ void group_tile(const StepArgs& A, double a, const Bi
   double s = 0.0;
   if (active)
     s = strided_sum<G, NT>(A.col, A.x_in, ld_stream<NT>(A.row_ptr + row),
-                           ld_stream<NT>(A.row_ptr + row + 1), gl);
+                           ld_stream<NT>(A.row_ptr + row + 1), gl, A.colmask);
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
   row_epilogue<MODE>(A, a, b.cls, row, s, active && gl == 0, lds);
+}
+
+// Sliced rows: the row sum is a fixed tree over the 8 slice partials.
+template <int MODE>
+__device__ __forceinline__ void combine_tile(const StepArgs& A, double a, const Bin& b,
+                                             uint32_t blk, uint64_t (*lds)[REC_WORDS]) {
+  const uint32_t i = blk * BLOCK + threadIdx.x;
+  const uint32_t row = b.row_begin + i;
+  const bool active = row < b.row_end;
+  double c = 0.0;
+  if (active) {
+    const uint32_t sr = b.srow_begin + i;
+    const double* p = A.part + sr;
+    const uint64_t S = A.nS;
+    c = ((p[0] + p[S]) + (p[2 * S] + p[3 * S])) + ((p[4 * S] + p[5 * S]) + (p[6 * S] + p[7 * S]));
+  }
+  row_epilogue<MODE>(A, a, b.cls, row, c, active, lds);
 }
 
 template <int MODE, int NT>
 __global__ __launch_bounds__(BLOCK) void spmv_round(StepArgs A) {
   __shared__ uint64_t lds[4][REC_WORDS];
   __shared__ double red[4];
-  const uint32_t b = blockIdx.x;
-  int lo = 0, hi = A.nbins - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (A.bins[mid].block_begin <= b) lo = mid; else hi = mid - 1;
-  }
-  const Bin bin = A.bins[lo];
+  const uint32_t b = blockIdx.x + A.block_base;
+  const Bin bin = A.bins[find_bin(A.bins, A.nbins, b)];
   const uint32_t blk = b - bin.block_begin;
   const double a = A.st->a;
   switch (bin.kind) {
@@ -303,20 +349,80 @@ __global__ __launch_bounds__(BLOCK) void spmv_round(StepArgs A) {
     case 4: group_tile<16, MODE, NT>(A, a, bin, blk, lds); break;
     case 5: group_tile<32, MODE, NT>(A, a, bin, blk, lds); break;
     case 6: group_tile<64, MODE, NT>(A, a, bin, blk, lds); break;
+    case KIND_COMBINE: combine_tile<MODE>(A, a, bin, blk, lds); break;
     case KIND_BLOCK: {
       const uint32_t row = bin.row_begin + blk;
       double s = strided_sum<BLOCK, NT>(A.col, A.x_in, A.row_ptr[row], A.row_ptr[row + 1],
-                                        threadIdx.x);
+                                        threadIdx.x, A.colmask);
       s = block_sum(s, red);
       row_epilogue<MODE>(A, a, bin.cls, row, s, threadIdx.x == 0, lds);
       break;
     }
-    default: {  // KIND_HUB: one segment of a split row -> partial (combined in hub_round)
-      const uint32_t sg = bin.seg_begin + blk;
-      const HubSeg seg = A.segs[sg];
-      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, seg.e_begin, seg.e_end, threadIdx.x);
+    default: {  // KIND_HUB: one segment of an unsliced split row (combined in hub_round)
+      const HubSeg seg = A.segs[bin.seg_begin + blk];
+      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, seg.e_begin, seg.e_end, threadIdx.x,
+                                        A.colmask);
       s = block_sum(s, red);
-      if (threadIdx.x == 0) A.hub_part[sg] = s;
+      if (threadIdx.x == 0) A.hub_part[seg.part] = s;
+      break;
+    }
+  }
+}
+
+// ---- the slice launch: grid = 8 x tiles, slice j = blockIdx % 8 (one XCD per slice) ----
+template <int G, int NT>
+__device__ __forceinline__ void slice_group(const StepArgs& A, const Bin& b, uint32_t blk,
+                                            uint32_t j) {
+  constexpr uint32_t RPB = BLOCK / G;
+  const uint32_t i = blk * RPB + threadIdx.x / G;
+  const uint32_t row = b.row_begin + i;
+  const int gl = threadIdx.x % G;
+  const bool active = row < b.row_end;
+  double s = 0.0;
+  const uint32_t sr = b.srow_begin + i;
+  if (active) {
+    const uint64_t base = ld_stream<NT>(A.row_ptr + row);
+    const uint64_t beg = base + ld_stream<NT>(A.sb + static_cast<uint64_t>(j) * A.nS + sr);
+    const uint64_t end = base + ld_stream<NT>(A.sb + static_cast<uint64_t>(j + 1) * A.nS + sr);
+    s = strided_sum<G, NT>(A.col, A.x_in, beg, end, gl, A.colmask);
+  }
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  if (active && gl == 0) A.part[static_cast<uint64_t>(j) * A.nS + sr] = s;
+}
+
+template <int NT>
+__global__ __launch_bounds__(BLOCK) void spmv_slices(StepArgs A) {
+  __shared__ double red[4];
+  const uint32_t b = blockIdx.x + A.block_base;
+  const uint32_t j = b % NSLICE, t = b / NSLICE;
+  const Bin bin = A.bins[find_bin(A.bins, A.nbins, t)];
+  const uint32_t blk = t - bin.block_begin;
+  switch (bin.kind) {
+    case 0: slice_group<1, NT>(A, bin, blk, j); break;
+    case 1: slice_group<2, NT>(A, bin, blk, j); break;
+    case 2: slice_group<4, NT>(A, bin, blk, j); break;
+    case 3: slice_group<8, NT>(A, bin, blk, j); break;
+    case 4: slice_group<16, NT>(A, bin, blk, j); break;
+    case 5: slice_group<32, NT>(A, bin, blk, j); break;
+    case 6: slice_group<64, NT>(A, bin, blk, j); break;
+    case KIND_BLOCK: {
+      const uint32_t row = bin.row_begin + blk;
+      const uint32_t sr = bin.srow_begin + blk;
+      const uint64_t base = A.row_ptr[row];
+      const uint64_t beg = base + A.sb[static_cast<uint64_t>(j) * A.nS + sr];
+      const uint64_t end = base + A.sb[static_cast<uint64_t>(j + 1) * A.nS + sr];
+      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, beg, end, threadIdx.x, A.colmask);
+      s = block_sum(s, red);
+      if (threadIdx.x == 0) A.part[static_cast<uint64_t>(j) * A.nS + sr] = s;
+      break;
+    }
+    default: {  // KIND_HUB: slice j's segment list (padded with empty segments)
+      const HubSeg seg = A.segs[static_cast<uint64_t>(j) * A.hub_tiles + bin.seg_begin + blk];
+      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, seg.e_begin, seg.e_end, threadIdx.x,
+                                        A.colmask);
+      s = block_sum(s, red);
+      if (threadIdx.x == 0 && seg.part != 0xFFFFFFFFu) A.hub_part[seg.part] = s;
       break;
     }
   }
@@ -504,11 +610,39 @@ __global__ void k_inverse(const uint32_t* perm, uint32_t n, uint32_t* inv) {
   if (k < n) inv[perm[k]] = k;
 }
 
+// rows dealt to ranks in chunks of CHUNK internal ids; slices by 128-byte x line
 struct Layout {
-  uint32_t p, nA, R, nC, maxA;
+  uint32_t p, rank, nA, R, nC, maxA;
+  uint32_t sm;        // slice-major x (p divides 8): every slice is one contiguous region
+  uint32_t SL, SLC;   // entries per slice region: class-A part / class-C part
 };
+__device__ __host__ __forceinline__ uint32_t owner_of(const Layout& L, uint32_t k) {
+  return (k / CHUNK) % L.p;
+}
+__device__ __host__ __forceinline__ uint32_t local_of(const Layout& L, uint32_t k) {
+  return ((k / CHUNK) / L.p) * CHUNK + (k % CHUNK);
+}
+__device__ __host__ __forceinline__ uint32_t row_of(const Layout& L, uint32_t l) {
+  return ((l / CHUNK) * L.p + L.rank) * CHUNK + (l % CHUNK);
+}
+// x position of column k.  Slice-major: A entries sit in the region of their owner rank,
+// inside it in the sub-region of their slice (chunk c = k>>4 has slice c&7 and, as p
+// divides 8, owner c%p = (c&7)%p), chunks of a slice in order -- each XCD's slice is one
+// contiguous, hotness-ordered address range (all L2 sets and channels in use).
 __device__ __forceinline__ uint32_t xpos(const Layout& L, uint32_t k) {
-  return k < L.nA ? (k % L.p) * L.maxA + k / L.p : L.p * L.maxA + (k - L.R);
+  if (k < L.nA) {
+    if (!L.sm) return owner_of(L, k) * L.maxA + local_of(L, k);
+    const uint32_t c = k / CHUNK, sl = c % NSLICE;
+    return (sl % L.p) * L.maxA + (sl / L.p) * L.SL + (c / NSLICE) * CHUNK + (k % CHUNK);
+  }
+  const uint32_t kc = k - L.R;
+  if (!L.sm) return L.p * L.maxA + kc;
+  const uint32_t c = kc / CHUNK;
+  return L.p * L.maxA + (c % NSLICE) * L.SLC + (c / NSLICE) * CHUNK + (kc % CHUNK);
+}
+// slice of a column = its 128-byte chunk index mod 8 (independent of the rank count)
+__device__ __forceinline__ uint32_t slice_of(const Layout& L, uint32_t k) {
+  return ((k < L.nA ? k : k - L.R) / CHUNK) % NSLICE;
 }
 
 __global__ void k_x_init(const uint32_t* perm, const uint32_t* outdeg, uint32_t n, Layout L,
@@ -519,21 +653,24 @@ __global__ void k_x_init(const uint32_t* perm, const uint32_t* outdeg, uint32_t 
   if (col) x_init[xpos(L, k)] = 1.0 / static_cast<double>(outdeg[perm[k]]);
 }
 
-// relabel unique edges to (local row, internal source) and keep this rank's rows
+// relabel unique edges to (local row, slice, internal source) and keep this rank's rows;
+// rows with in-degree >= ks get their edges grouped by the slice of the source's x line
 __global__ void k_relabel(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv,
-                          uint32_t p, uint32_t rank, unsigned long long* counter,
-                          uint64_t* out) {
+                          const uint32_t* indeg, uint32_t ks, Layout L,
+                          unsigned long long* counter, uint64_t* out) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   bool keep = false;
   uint64_t key = 0;
   if (e < nnz) {
     const uint64_t k = uk[e];
-    const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
-    const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
-    keep = (kd % p) == rank;
-    key = (static_cast<uint64_t>(kd / p) << nb) | ks;
+    const uint32_t d = static_cast<uint32_t>(k >> nb);
+    const uint32_t kd = inv[d];
+    const uint32_t ksrc = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
+    keep = owner_of(L, kd) == L.rank;
+    const uint64_t sl = indeg[d] >= ks ? slice_of(L, ksrc) : 0u;
+    key = (static_cast<uint64_t>(local_of(L, kd)) << (nb + 3)) | (sl << nb) | ksrc;
   }
-  if (p == 1) {
+  if (L.p == 1) {
     if (e < nnz) out[e] = key;
     return;
   }
@@ -548,21 +685,54 @@ __global__ void k_relabel(const uint64_t* uk, uint64_t nnz, int nb, const uint32
   if (keep) out[base + __popcll(mask & ((1ull << lane) - 1))] = key;
 }
 
-__global__ void k_col(const uint64_t* lk, uint64_t lnnz, int nb, Layout L, uint32_t* col) {
+struct SliceRows {
+  uint32_t lA, sA, sB, nS;
+};
+__device__ __forceinline__ int srow_of(const SliceRows& S, uint32_t l) {
+  if (l < S.sA) return static_cast<int>(l);
+  if (l >= S.lA && l - S.lA < S.sB) return static_cast<int>(S.sA + (l - S.lA));
+  return -1;
+}
+
+// col = x position of the source; per (sliced row, slice) edge counts
+__global__ void k_col(const uint64_t* lk, uint64_t lnnz, int nb, Layout L, SliceRows S,
+                      uint32_t hot, uint32_t* col, uint32_t* cnt) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (e < lnnz) col[e] = xpos(L, static_cast<uint32_t>(lk[e] & ((1ull << nb) - 1)));
+  if (e >= lnnz) return;
+  const uint64_t key = lk[e];
+  const uint32_t ksrc = static_cast<uint32_t>(key & ((1ull << nb) - 1));
+  // cold = beyond the first `hot` entries of the source's slice region (slice-major only)
+  const bool cold = L.sm && (ksrc >= L.nA || (ksrc / CHUNK) / NSLICE * CHUNK >= hot);
+  col[e] = xpos(L, ksrc) | (cold ? 0x80000000u : 0u);
+  const int sr = srow_of(S, static_cast<uint32_t>(key >> (nb + 3)));
+  if (sr >= 0) {
+    const uint32_t sl = static_cast<uint32_t>((key >> nb) & 7);
+    atomicAdd(&cnt[static_cast<uint64_t>(sl) * S.nS + sr], 1u);
+  }
+}
+
+// sb[j][srow] = edges of the row in slices < j (relative to the row start)
+__global__ void k_slice_prefix(const uint32_t* cnt, uint32_t nS, uint32_t* sb) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nS) return;
+  uint32_t acc = 0;
+  for (int j = 0; j < NSLICE; ++j) {
+    sb[static_cast<uint64_t>(j) * nS + r] = acc;
+    acc += cnt[static_cast<uint64_t>(j) * nS + r];
+  }
+  sb[static_cast<uint64_t>(NSLICE) * nS + r] = acc;
 }
 
 __global__ void k_local_rows(const uint32_t* perm, const uint32_t* indeg, const uint32_t* outdeg,
-                             const uint32_t* dang_w, uint32_t lrows, uint32_t lA, uint32_t p,
-                             uint32_t rank, uint64_t* deg64, uint32_t* ldeg, uint32_t* meta) {
+                             const uint32_t* dang_w, uint32_t lrows, uint32_t lA, Layout L,
+                             uint64_t* deg64, uint32_t* ldeg, uint32_t* meta) {
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l > lrows) return;
   if (l == lrows) {
     deg64[l] = 0;
     return;
   }
-  const uint32_t v = perm[l * p + rank];
+  const uint32_t v = perm[row_of(L, l)];
   const uint32_t d = indeg[v];
   deg64[l] = d;
   ldeg[l] = d;
@@ -570,9 +740,9 @@ __global__ void k_local_rows(const uint32_t* perm, const uint32_t* indeg, const 
 }
 
 __global__ void k_scatter_ranks(const uint32_t* perm, const double* r_loc, uint32_t lrows,
-                                uint32_t p, uint32_t rank, double* r_full) {
+                                Layout L, double* r_full) {
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l < lrows) r_full[perm[l * p + rank]] = r_loc[l];
+  if (l < lrows) r_full[perm[row_of(L, l)]] = r_loc[l];
 }
 
 __global__ void k_sources_one(const uint32_t* outdeg, uint32_t n, double* r_full) {
@@ -631,34 +801,69 @@ int env_int(const char* name, int def) {
 void dev_free(DevGraph* g) {
   auto F = [](void* p) { if (p) (void)hipFree(p); };
   F(g->row_ptr); F(g->col); F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
+  F(g->sb); F(g->part);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
-  F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->d_bins); F(g->d_hubs);
-  F(g->d_segs); F(g->hub_part);
+  F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->d_bins); F(g->d_sbins);
+  F(g->d_hubs); F(g->d_segs); F(g->d_ssegs); F(g->hub_part);
+  for (auto e : g->split_ev) (void)hipEventDestroy(e);
   const int p = g->p, rank = g->rank;
   *g = DevGraph();
   g->p = p;
   g->rank = rank;
 }
 
+namespace {
+
+Layout layout_of(const DevGraph* g) {
+  return Layout{static_cast<uint32_t>(g->p), static_cast<uint32_t>(g->rank), g->nA, g->R, g->nC,
+                g->maxA, g->sm ? 1u : 0u, g->SL, g->SLC};
+}
+
+// rows owned by rank j among internal ids [0, cnt) when chunks of CHUNK are dealt round-robin
+uint32_t owned_rows(uint32_t cnt, uint32_t p, uint32_t j) {
+  const uint32_t full = cnt / CHUNK, rem = cnt % CHUNK;
+  uint32_t r = CHUNK * (full / p + (j < full % p ? 1u : 0u));
+  if (rem && full % p == j) r += rem;
+  return r;
+}
+
+uint16_t kind_for(uint64_t len, const Tuning& T) {
+  if (len > T.kb) return KIND_BLOCK;
+  const uint64_t want = (len + T.epl - 1) / T.epl;
+  uint16_t kd = 0;
+  while ((1ull << kd) < want && kd < 6) ++kd;
+  return kd;
+}
+
+}  // namespace
+
 int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err) {
   auto t0 = std::chrono::steady_clock::now();
   const int p = g->p, rank = g->rank;
   dev_free(g);
-  g->tune.epl = std::max(1, env_int("PR_EPL", g->tune.epl));
-  g->tune.kb = static_cast<uint32_t>(std::max(64, env_int("PR_KB", static_cast<int>(g->tune.kb))));
-  g->tune.kh = static_cast<uint32_t>(std::max(static_cast<int>(g->tune.kb), env_int("PR_KH", static_cast<int>(g->tune.kh))));
-  g->tune.seg = static_cast<uint32_t>(std::max(256, env_int("PR_SEG", static_cast<int>(g->tune.seg))));
-  g->tune.nt = env_int("PR_NT", g->tune.nt);
+  Tuning& T = g->tune;
+  T.epl = std::max(1, env_int("PR_EPL", T.epl));
+  T.kb = static_cast<uint32_t>(std::max(64, env_int("PR_KB", static_cast<int>(T.kb))));
+  T.kh = static_cast<uint32_t>(std::max(static_cast<int>(T.kb), env_int("PR_KH", static_cast<int>(T.kh))));
+  T.seg = static_cast<uint32_t>(std::max(256, env_int("PR_SEG", static_cast<int>(T.seg))));
+  T.ks = static_cast<uint32_t>(std::max(1, env_int("PR_KS", static_cast<int>(T.ks))));
+  T.nt = env_int("PR_NT", T.nt);
+  T.hot = static_cast<uint32_t>(env_int("PR_HOT", static_cast<int>(T.hot)));
+  T.split = env_int("PR_SPLIT", 0);
+  if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   const uint32_t n = in.n;
   const uint64_t m = in.m;
   g->n = n;
   g->m_raw = m;
   g->n_tot = in.n_tot;
   const int nb = in.rmat ? std::max(1, in.scale) : bits_for(n);
-  if (2 * nb > 64) {
-    if (err) *err = "vertex count too large for 64-bit edge keys";
+  // edge keys (local row, slice, source) take 2*nb + 3 bits
+  if (2 * nb + 3 > 64) {
+    if (err) *err = "more than 2^30 vertices is not supported (64-bit edge keys)";
     return PR_E_ARG;
   }
+  const uint32_t ks = T.ks;
+  const int key_bits = 2 * nb + 3;
   Temp tmp;
 
   // ---- raw keys (dst << nb | src) ------------------------------------------------------
@@ -759,7 +964,6 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   g->digest[1] = sums[1];
   g->W0 = sums[2];
   g->n_dang_entries = sums[2];
-  // class sizes from the first index of each class (absent class: starts where next starts)
   uint32_t start[5];
   start[4] = n;
   for (int c = 3; c >= 0; --c) start[c] = cls_first[c] == 0xFFFFFFFFu ? start[c + 1] : cls_first[c];
@@ -769,54 +973,40 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   g->nD = start[4] - start[3];
   g->R = g->nA + g->nB;
   const uint32_t P = static_cast<uint32_t>(p), RK = static_cast<uint32_t>(rank);
-  g->maxA = (g->nA + P - 1) / P;
-  g->X = static_cast<uint64_t>(P) * g->maxA + g->nC;
-  auto owned = [&](uint32_t cnt) -> uint32_t { return cnt > RK ? (cnt - RK + P - 1) / P : 0u; };
-  g->lrows = owned(g->R);
-  g->lA = owned(g->nA);
-  const Layout L{P, g->nA, g->R, g->nC, g->maxA};
+  g->sm = (NSLICE % P) == 0 && env_int("PR_SLICE_MAJOR", 1) != 0;
+  if (g->sm) {
+    const uint32_t chA = (g->nA + CHUNK - 1) / CHUNK, chC = (g->nC + CHUNK - 1) / CHUNK;
+    g->SL = CHUNK * ((chA + NSLICE - 1) / NSLICE);
+    g->SLC = CHUNK * ((chC + NSLICE - 1) / NSLICE);
+    g->maxA = (NSLICE / P) * g->SL;
+    g->X = static_cast<uint64_t>(P) * g->maxA + static_cast<uint64_t>(NSLICE) * g->SLC;
+  } else {
+    uint32_t maxA = 0;
+    for (uint32_t j = 0; j < P; ++j) maxA = std::max(maxA, owned_rows(g->nA, P, j));
+    g->maxA = (maxA + CHUNK - 1) / CHUNK * CHUNK;
+    g->X = static_cast<uint64_t>(P) * g->maxA + g->nC;
+  }
+  g->lrows = owned_rows(g->R, P, RK);
+  g->lA = owned_rows(g->nA, P, RK);
+  const Layout L = layout_of(g);
 
   // ---- x vectors ------------------------------------------------------------------------
-  TRY(dmalloc(&g->x_init, g->X, err));
-  TRY(dmalloc(&g->xbuf[0], g->X, err));
-  TRY(dmalloc(&g->xbuf[1], g->X, err));
+  if (env_int("PR_XUNCACHED", 0)) {  // experiment: x in uncached device memory (32-B reads)
+    for (double** px : {&g->x_init, &g->xbuf[0], &g->xbuf[1]})
+      HIPTRY(hipExtMallocWithFlags(reinterpret_cast<void**>(px), 8 * (g->X ? g->X : 1), hipDeviceMallocUncached));
+  } else {
+    TRY(dmalloc(&g->x_init, g->X, err));
+    TRY(dmalloc(&g->xbuf[0], g->X, err));
+    TRY(dmalloc(&g->xbuf[1], g->X, err));
+  }
   HIPTRY(hipMemsetAsync(g->x_init, 0, 8 * (g->X ? g->X : 1), s));
   HIPTRY(hipMemsetAsync(g->xbuf[0], 0, 8 * (g->X ? g->X : 1), s));
   HIPTRY(hipMemsetAsync(g->xbuf[1], 0, 8 * (g->X ? g->X : 1), s));
   if (n) hipLaunchKernelGGL(k_x_init, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->perm, g->outdeg, n, L, g->x_init);
-  uint32_t* inv = reinterpret_cast<uint32_t*>(vid);  // reuse: n entries
+  uint32_t* inv = vid;  // reuse: n entries
   if (n) hipLaunchKernelGGL(k_inverse, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->perm, n, inv);
 
-  // ---- local edges: relabel, keep own rows, sort by (local row, internal source) --------
-  uint64_t* lk_in = uniq == kA ? kB : kA;  // free buffer
-  unsigned long long* d_lc = nullptr;
-  TRY(dmalloc(&d_lc, 1, err));
-  HIPTRY(hipMemsetAsync(d_lc, 0, 8, s));
-  if (nnz) hipLaunchKernelGGL(k_relabel, dim3(grid_for(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, P, RK, d_lc, lk_in);
-  uint64_t lnnz = nnz;
-  if (p > 1) {
-    HIPTRY(hipMemcpyAsync(&lnnz, d_lc, 8, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipStreamSynchronize(s));
-  }
-  (void)hipFree(d_lc);
-  g->lnnz = lnnz;
-  uint64_t* lk_sorted = nullptr;
-  {
-    rocprim::double_buffer<uint64_t> db(lk_in, uniq);
-    size_t tb = 0;
-    HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, lnnz, 0, 2 * nb, s));
-    TRY(tmp.ensure(tb, err));
-    if (lnnz) HIPTRY(rocprim::radix_sort_keys(tmp.p, tb, db, lnnz, 0, 2 * nb, s));
-    lk_sorted = db.current();
-  }
-  TRY(dmalloc(&g->col, lnnz, err));
-  if (lnnz) hipLaunchKernelGGL(k_col, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk_sorted, lnnz, nb, L, g->col);
-  HIPTRY(hipStreamSynchronize(s));
-  (void)hipFree(kA);
-  (void)hipFree(kB);
-  kA = kB = nullptr;
-
-  // ---- row pointers + per-row meta -------------------------------------------------------
+  // ---- per-row data: in-degrees (host copy for the schedule), meta, row pointers --------
   const uint32_t lrows = g->lrows;
   uint64_t* deg64 = nullptr;
   uint32_t* ldeg = nullptr;
@@ -824,7 +1014,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&ldeg, lrows, err));
   TRY(dmalloc(&g->meta, lrows, err));
   TRY(dmalloc(&g->row_ptr, lrows + 1ull, err));
-  hipLaunchKernelGGL(k_local_rows, dim3(grid_for(lrows + 1ull)), dim3(BLOCK), 0, s, g->perm, g->indeg, g->outdeg, g->dang_w, lrows, g->lA, P, RK, deg64, ldeg, g->meta);
+  hipLaunchKernelGGL(k_local_rows, dim3(grid_for(lrows + 1ull)), dim3(BLOCK), 0, s, g->perm, g->indeg, g->outdeg, g->dang_w, lrows, g->lA, L, deg64, ldeg, g->meta);
   {
     size_t tb = 0;
     HIPTRY(rocprim::exclusive_scan(nullptr, tb, deg64, g->row_ptr, uint64_t(0), lrows + 1ull, rocprim::plus<uint64_t>(), s));
@@ -836,73 +1026,205 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   HIPTRY(hipStreamSynchronize(s));
   (void)hipFree(deg64);
   (void)hipFree(ldeg);
-  (void)hipFree(vid);
-
-  // ---- schedule: degree bins over [0,lA) (class A) and [lA,lrows) (class B) -------------
-  // rows are sorted by in-degree (descending) inside each class, so each kind is one run.
-  auto kind_of = [&](uint32_t k) -> uint16_t {
-    if (k > g->tune.kh) return KIND_HUB;
-    if (k > g->tune.kb) return KIND_BLOCK;
-    const uint32_t want = (k + g->tune.epl - 1) / g->tune.epl;
-    uint16_t kd = 0;
-    while ((1u << kd) < want && kd < 6) ++kd;
-    return kd;
-  };
   std::vector<uint64_t> hrow(lrows + 1ull, 0);
   for (uint32_t l = 0; l < lrows; ++l) hrow[l + 1] = hrow[l] + hdeg[l];
-  struct Run { uint16_t kind, cls; uint32_t b, e; };
-  std::vector<Run> runs;
-  for (int cls = 0; cls < 2; ++cls) {
-    const uint32_t b0 = cls ? g->lA : 0, e0 = cls ? lrows : g->lA;
-    uint32_t i = b0;
-    while (i < e0) {
-      const uint16_t kd = kind_of(hdeg[i]);
-      uint32_t j = i + 1;
-      while (j < e0 && kind_of(hdeg[j]) == kd) ++j;
-      runs.push_back({kd, static_cast<uint16_t>(cls), i, j});
-      i = j;
-    }
+  // rows are sorted by in-degree (descending) inside each class: sliced rows and hubs lead
+  auto lead = [&](uint32_t b, uint32_t e, uint64_t thr) {
+    uint32_t i = b;
+    while (i < e && hdeg[i] >= thr) ++i;
+    return i - b;
+  };
+  g->sA = lead(0, g->lA, ks);
+  g->sB = lead(g->lA, lrows, ks);
+  g->hA = std::min(g->sA, lead(0, g->lA, T.kh + 1ull));
+  g->hB = std::min(g->sB, lead(g->lA, lrows, T.kh + 1ull));
+  g->nS = g->sA + g->sB;
+  const SliceRows SR{g->lA, g->sA, g->sB, g->nS};
+
+  // ---- local edges: relabel, keep own rows, sort by (local row, slice, source) ----------
+  uint64_t* lk_in = uniq == kA ? kB : kA;  // free buffer
+  unsigned long long* d_lc = nullptr;
+  TRY(dmalloc(&d_lc, 1, err));
+  HIPTRY(hipMemsetAsync(d_lc, 0, 8, s));
+  if (nnz) hipLaunchKernelGGL(k_relabel, dim3(grid_for(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, g->indeg, ks, L, d_lc, lk_in);
+  uint64_t lnnz = nnz;
+  if (p > 1) {
+    HIPTRY(hipMemcpyAsync(&lnnz, d_lc, 8, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
   }
-  // heavy kinds first so long rows start early
-  std::stable_sort(runs.begin(), runs.end(), [](const Run& a, const Run& b) {
-    return a.kind > b.kind;
-  });
-  std::vector<HubSeg> segs;
-  uint32_t blocks = 0;
-  for (const Run& r : runs) {
-    Bin b{};
-    b.block_begin = blocks;
-    b.row_begin = r.b;
-    b.row_end = r.e;
-    b.kind = r.kind;
-    b.cls = r.cls;
-    b.seg_begin = static_cast<uint32_t>(segs.size());
-    if (r.kind == KIND_HUB) {
-      for (uint32_t l = r.b; l < r.e; ++l) {
-        HubRow h{l, static_cast<uint32_t>(segs.size()), 0, r.cls};
-        for (uint64_t e = hrow[l]; e < hrow[l + 1]; e += g->tune.seg)
-          segs.push_back({e, std::min<uint64_t>(e + g->tune.seg, hrow[l + 1])});
-        h.part_end = static_cast<uint32_t>(segs.size());
-        g->hubs.push_back(h);
+  (void)hipFree(d_lc);
+  g->lnnz = lnnz;
+  uint64_t* lk_sorted = nullptr;
+  {
+    rocprim::double_buffer<uint64_t> db(lk_in, uniq);
+    size_t tb = 0;
+    HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, lnnz, 0, key_bits, s));
+    TRY(tmp.ensure(tb, err));
+    if (lnnz) HIPTRY(rocprim::radix_sort_keys(tmp.p, tb, db, lnnz, 0, key_bits, s));
+    lk_sorted = db.current();
+  }
+  TRY(dmalloc(&g->col, lnnz, err));
+  uint32_t* cnt = nullptr;
+  TRY(dmalloc(&cnt, static_cast<size_t>(NSLICE) * g->nS, err));
+  if (g->nS) HIPTRY(hipMemsetAsync(cnt, 0, 4ull * NSLICE * g->nS, s));
+  if (lnnz) hipLaunchKernelGGL(k_col, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk_sorted, lnnz, nb, L, SR, T.hot, g->col, cnt);
+  TRY(dmalloc(&g->sb, (NSLICE + 1ull) * g->nS, err));
+  if (g->nS) hipLaunchKernelGGL(k_slice_prefix, dim3(grid_for(g->nS)), dim3(BLOCK), 0, s, cnt, g->nS, g->sb);
+  HIPTRY(hipStreamSynchronize(s));
+  HIPTRY(hipGetLastError());
+  (void)hipFree(cnt);
+  (void)hipFree(kA);
+  (void)hipFree(kB);
+  kA = kB = nullptr;
+  (void)hipFree(vid);
+  TRY(dmalloc(&g->part, static_cast<size_t>(NSLICE) * g->nS, err));
+
+  // ---- schedule ---------------------------------------------------------------------------
+  // hub rows' slice offsets on the host (sliced hubs are split per slice into segments)
+  std::vector<uint32_t> hsb;  // [9][hA+hB]
+  const uint32_t nh_s = g->hA + g->hB;
+  if (nh_s) {
+    hsb.resize((NSLICE + 1ull) * nh_s);
+    for (int j = 0; j <= NSLICE; ++j) {
+      if (g->hA) HIPTRY(hipMemcpyAsync(&hsb[j * nh_s], g->sb + static_cast<uint64_t>(j) * g->nS, 4ull * g->hA, hipMemcpyDeviceToHost, s));
+      if (g->hB) HIPTRY(hipMemcpyAsync(&hsb[j * nh_s + g->hA], g->sb + static_cast<uint64_t>(j) * g->nS + g->sA, 4ull * g->hB, hipMemcpyDeviceToHost, s));
+    }
+    HIPTRY(hipStreamSynchronize(s));
+  }
+  uint32_t next_part = 0;
+  // (a) slice launch over sliced rows: kinds by the expected per-slice length k/8
+  {
+    std::vector<std::vector<HubSeg>> lists(NSLICE);
+    uint32_t tiles = 0, hub_tiles = 0;
+    for (int cls = 0; cls < 2; ++cls) {
+      const uint32_t r0 = cls ? g->lA : 0;
+      const uint32_t nsl = cls ? g->sB : g->sA, nhub = cls ? g->hB : g->hA;
+      const uint32_t srow0 = cls ? g->sA : 0, hub_i0 = cls ? g->hA : 0;
+      if (nhub) {  // hub rows: per-slice segment lists, padded to equal length
+        Bin b{};
+        b.block_begin = tiles;
+        b.row_begin = r0;
+        b.row_end = r0 + nhub;
+        b.kind = KIND_HUB;
+        b.cls = static_cast<uint16_t>(cls);
+        b.seg_begin = hub_tiles;
+        b.srow_begin = srow0;
+        size_t before[NSLICE];
+        for (int j = 0; j < NSLICE; ++j) before[j] = lists[j].size();
+        for (uint32_t i = 0; i < nhub; ++i) {
+          const uint32_t l = r0 + i;
+          HubRow h{l, next_part, 0, static_cast<uint32_t>(cls)};
+          for (int j = 0; j < NSLICE; ++j) {
+            const uint64_t e0 = hrow[l] + hsb[j * nh_s + hub_i0 + i];
+            const uint64_t e1 = hrow[l] + hsb[(j + 1) * nh_s + hub_i0 + i];
+            for (uint64_t e = e0; e < e1; e += T.seg)
+              lists[j].push_back({e, std::min<uint64_t>(e + T.seg, e1), next_part++, 0});
+          }
+          h.part_end = next_part;
+          g->hubs.push_back(h);
+        }
+        size_t T_ = 0;
+        for (int j = 0; j < NSLICE; ++j) T_ = std::max(T_, lists[j].size() - before[j]);
+        for (int j = 0; j < NSLICE; ++j)
+          while (lists[j].size() - before[j] < T_) lists[j].push_back({0, 0, 0xFFFFFFFFu, 0});
+        tiles += static_cast<uint32_t>(T_);
+        hub_tiles += static_cast<uint32_t>(T_);
+        g->sbins.push_back(b);
+        g->sbin_edges.push_back(hrow[r0 + nhub] - hrow[r0]);
       }
-      blocks += static_cast<uint32_t>(segs.size()) - b.seg_begin;
-    } else if (r.kind == KIND_BLOCK) {
-      blocks += r.e - r.b;
-    } else {
-      const uint32_t rpb = BLOCK >> r.kind;
-      blocks += (r.e - r.b + rpb - 1) / rpb;
+      uint32_t i = nhub;
+      while (i < nsl) {  // non-hub sliced rows: runs of equal kind
+        const uint16_t kd = kind_for((hdeg[r0 + i] + NSLICE - 1) / NSLICE, T);
+        uint32_t e = i + 1;
+        while (e < nsl && kind_for((hdeg[r0 + e] + NSLICE - 1) / NSLICE, T) == kd) ++e;
+        Bin b{};
+        b.block_begin = tiles;
+        b.row_begin = r0 + i;
+        b.row_end = r0 + e;
+        b.kind = kd;
+        b.cls = static_cast<uint16_t>(cls);
+        b.srow_begin = srow0 + i;
+        const uint32_t rows = e - i;
+        tiles += kd == KIND_BLOCK ? rows : (rows + (BLOCK >> kd) - 1) / (BLOCK >> kd);
+        g->sbins.push_back(b);
+        g->sbin_edges.push_back(hrow[r0 + e] - hrow[r0 + i]);
+        i = e;
+      }
     }
-    g->bins.push_back(b);
+    g->slice_tiles = tiles;
+    g->hub_tiles = hub_tiles;
+    std::vector<HubSeg> flat(static_cast<size_t>(NSLICE) * hub_tiles);
+    for (int j = 0; j < NSLICE; ++j)
+      for (uint32_t t = 0; t < hub_tiles; ++t) flat[static_cast<size_t>(j) * hub_tiles + t] = lists[j][t];
+    TRY(dmalloc(&g->d_ssegs, flat.size(), err));
+    if (!flat.empty()) HIPTRY(hipMemcpyAsync(g->d_ssegs, flat.data(), flat.size() * sizeof(HubSeg), hipMemcpyHostToDevice, s));
+    TRY(dmalloc(&g->d_sbins, g->sbins.size(), err));
+    if (!g->sbins.empty()) HIPTRY(hipMemcpyAsync(g->d_sbins, g->sbins.data(), g->sbins.size() * sizeof(Bin), hipMemcpyHostToDevice, s));
   }
-  g->total_blocks = blocks;
-  g->n_parts = static_cast<uint32_t>(segs.size());
-  TRY(dmalloc(&g->d_bins, g->bins.size(), err));
-  if (!g->bins.empty()) HIPTRY(hipMemcpyAsync(g->d_bins, g->bins.data(), g->bins.size() * sizeof(Bin), hipMemcpyHostToDevice, s));
-  TRY(dmalloc(&g->d_segs, segs.size(), err));
-  if (!segs.empty()) HIPTRY(hipMemcpyAsync(g->d_segs, segs.data(), segs.size() * sizeof(HubSeg), hipMemcpyHostToDevice, s));
+  // (b) row launch: combine bins for sliced non-hub rows, then unsliced rows by kind
+  {
+    struct Run { uint16_t kind, cls; uint32_t b, e, srow; };
+    std::vector<Run> runs;
+    for (int cls = 0; cls < 2; ++cls) {
+      const uint32_t r0 = cls ? g->lA : 0;
+      const uint32_t nsl = cls ? g->sB : g->sA, nhub = cls ? g->hB : g->hA;
+      const uint32_t srow0 = cls ? g->sA : 0;
+      if (nsl > nhub) runs.push_back({KIND_COMBINE, static_cast<uint16_t>(cls), r0 + nhub, r0 + nsl, srow0 + nhub});
+      const uint32_t e0 = cls ? lrows : g->lA;
+      uint32_t i = r0 + nsl;
+      while (i < e0) {
+        const uint16_t kd = hdeg[i] > T.kh ? static_cast<uint16_t>(KIND_HUB) : kind_for(hdeg[i], T);
+        uint32_t e = i + 1;
+        while (e < e0 && (hdeg[e] > T.kh ? static_cast<uint16_t>(KIND_HUB) : kind_for(hdeg[e], T)) == kd) ++e;
+        runs.push_back({kd, static_cast<uint16_t>(cls), i, e, 0});
+        i = e;
+      }
+    }
+    std::stable_sort(runs.begin(), runs.end(), [](const Run& a, const Run& b) {
+      auto w = [](uint16_t k) { return k == KIND_COMBINE ? 100 : static_cast<int>(k); };
+      return w(a.kind) > w(b.kind);
+    });
+    std::vector<HubSeg> segs;
+    uint32_t blocks = 0;
+    for (const Run& r : runs) {
+      Bin b{};
+      b.block_begin = blocks;
+      b.row_begin = r.b;
+      b.row_end = r.e;
+      b.kind = r.kind;
+      b.cls = r.cls;
+      b.srow_begin = r.srow;
+      b.seg_begin = static_cast<uint32_t>(segs.size());
+      if (r.kind == KIND_HUB) {
+        for (uint32_t l = r.b; l < r.e; ++l) {
+          HubRow h{l, next_part, 0, r.cls};
+          for (uint64_t e = hrow[l]; e < hrow[l + 1]; e += T.seg)
+            segs.push_back({e, std::min<uint64_t>(e + T.seg, hrow[l + 1]), next_part++, 0});
+          h.part_end = next_part;
+          g->hubs.push_back(h);
+        }
+        blocks += static_cast<uint32_t>(segs.size()) - b.seg_begin;
+      } else if (r.kind == KIND_BLOCK) {
+        blocks += r.e - r.b;
+      } else if (r.kind == KIND_COMBINE) {
+        blocks += (r.e - r.b + BLOCK - 1) / BLOCK;
+      } else {
+        const uint32_t rpb = BLOCK >> r.kind;
+        blocks += (r.e - r.b + rpb - 1) / rpb;
+      }
+      g->bins.push_back(b);
+      g->bin_edges.push_back(hrow[r.e] - hrow[r.b]);
+    }
+    g->total_blocks = blocks;
+    TRY(dmalloc(&g->d_bins, g->bins.size(), err));
+    if (!g->bins.empty()) HIPTRY(hipMemcpyAsync(g->d_bins, g->bins.data(), g->bins.size() * sizeof(Bin), hipMemcpyHostToDevice, s));
+    TRY(dmalloc(&g->d_segs, segs.size(), err));
+    if (!segs.empty()) HIPTRY(hipMemcpyAsync(g->d_segs, segs.data(), segs.size() * sizeof(HubSeg), hipMemcpyHostToDevice, s));
+  }
+  g->n_parts = next_part;
   TRY(dmalloc(&g->d_hubs, g->hubs.size(), err));
   if (!g->hubs.empty()) HIPTRY(hipMemcpyAsync(g->d_hubs, g->hubs.data(), g->hubs.size() * sizeof(HubRow), hipMemcpyHostToDevice, s));
-  TRY(dmalloc(&g->hub_part, segs.size(), err));
+  TRY(dmalloc(&g->hub_part, next_part, err));
 
   // ---- iteration buffers ----------------------------------------------------------------
   TRY(dmalloc(&g->r_loc[0], lrows, err));
@@ -934,12 +1256,35 @@ int dev_reset_state(DevGraph* g, hipStream_t s) {
 
 double* dev_x_out(DevGraph* g, int t) { return g->xbuf[(t - 1) & 1]; }
 
+namespace {
+
+// launch helpers for both grids (template dispatch on MODE / NT)
+void launch_rows(const DevGraph* g, StepArgs A, int mode, uint32_t base, uint32_t nblk,
+                 hipStream_t s) {
+  A.block_base = base;
+  const dim3 gr(nblk), bl(BLOCK);
+  if (g->tune.nt) {
+    if (mode == 0) hipLaunchKernelGGL((spmv_round<0, 1>), gr, bl, 0, s, A);
+    else if (mode == 1) hipLaunchKernelGGL((spmv_round<1, 1>), gr, bl, 0, s, A);
+    else hipLaunchKernelGGL((spmv_round<2, 1>), gr, bl, 0, s, A);
+  } else {
+    if (mode == 0) hipLaunchKernelGGL((spmv_round<0, 0>), gr, bl, 0, s, A);
+    else if (mode == 1) hipLaunchKernelGGL((spmv_round<1, 0>), gr, bl, 0, s, A);
+    else hipLaunchKernelGGL((spmv_round<2, 0>), gr, bl, 0, s, A);
+  }
+}
+void launch_slices(const DevGraph* g, StepArgs A, uint32_t base, uint32_t nblk, hipStream_t s) {
+  A.block_base = base;
+  if (g->tune.nt) hipLaunchKernelGGL((spmv_slices<1>), dim3(nblk), dim3(BLOCK), 0, s, A);
+  else hipLaunchKernelGGL((spmv_slices<0>), dim3(nblk), dim3(BLOCK), 0, s, A);
+}
+
+}  // namespace
+
 int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev0,
                       hipEvent_t ev1) {
   std::string* err = nullptr;
   StepArgs A{};
-  A.bins = g->d_bins;
-  A.nbins = static_cast<int>(g->bins.size());
   A.row_ptr = g->row_ptr;
   A.col = g->col;
   A.meta = g->meta;
@@ -947,23 +1292,58 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.x_out = dev_x_out(g, t) + static_cast<uint64_t>(g->rank) * g->maxA;
   A.r_old = t == 1 ? nullptr : g->r_loc[(t - 1) & 1];
   A.r_out = g->r_loc[t & 1];
-  A.segs = g->d_segs;
   A.hub_part = g->hub_part;
   A.hubs = g->d_hubs;
   A.st = g->state;
   A.shards = g->shards;
+  A.sb = g->sb;
+  A.part = g->part;
+  A.nS = g->nS;
+  A.hub_tiles = g->hub_tiles;
+  A.colmask = g->tune.colmask;
+  A.p = static_cast<uint32_t>(g->p);
+  A.rank = static_cast<uint32_t>(g->rank);
+  A.sm = g->sm ? 1u : 0u;
+  A.SL = g->SL;
+  StepArgs AS = A;  // slice launch
+  AS.bins = g->d_sbins;
+  AS.nbins = static_cast<int>(g->sbins.size());
+  AS.segs = g->d_ssegs;
+  A.bins = g->d_bins;
+  A.nbins = static_cast<int>(g->bins.size());
+  A.segs = g->d_segs;
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
-  if (g->total_blocks) {
-    const dim3 gr(g->total_blocks), bl(BLOCK);
-    if (g->tune.nt) {
-      if (mode == 0) hipLaunchKernelGGL((spmv_round<0, 1>), gr, bl, 0, s, A);
-      else if (mode == 1) hipLaunchKernelGGL((spmv_round<1, 1>), gr, bl, 0, s, A);
-      else hipLaunchKernelGGL((spmv_round<2, 1>), gr, bl, 0, s, A);
-    } else {
-      if (mode == 0) hipLaunchKernelGGL((spmv_round<0, 0>), gr, bl, 0, s, A);
-      else if (mode == 1) hipLaunchKernelGGL((spmv_round<1, 0>), gr, bl, 0, s, A);
-      else hipLaunchKernelGGL((spmv_round<2, 0>), gr, bl, 0, s, A);
+  if (g->tune.split) {
+    // timing mode: one launch per bin, each bracketed by events (DevGraph::split_ms)
+    const size_t nsb = g->sbins.size(), nrb = g->bins.size();
+    if (g->split_ev.empty()) {
+      g->split_ev.resize(2 * (nsb + nrb));
+      for (auto& e : g->split_ev) HIPTRY(hipEventCreate(&e));
+      g->split_ms.assign(nsb + nrb, 0.0);
     }
+    for (size_t i = 0; i < nsb + nrb; ++i) {
+      const bool sl = i < nsb;
+      const std::vector<Bin>& bv = sl ? g->sbins : g->bins;
+      const size_t k = sl ? i : i - nsb;
+      const uint32_t tot = sl ? g->slice_tiles : g->total_blocks;
+      const uint32_t b0 = bv[k].block_begin;
+      const uint32_t b1 = k + 1 < bv.size() ? bv[k + 1].block_begin : tot;
+      HIPTRY(hipEventRecord(g->split_ev[2 * i], s));
+      if (b1 > b0) {
+        if (sl) launch_slices(g, AS, NSLICE * b0, NSLICE * (b1 - b0), s);
+        else launch_rows(g, A, mode, b0, b1 - b0, s);
+      }
+      HIPTRY(hipEventRecord(g->split_ev[2 * i + 1], s));
+    }
+    HIPTRY(hipStreamSynchronize(s));
+    for (size_t i = 0; i < nsb + nrb; ++i) {
+      float ms = 0.f;
+      HIPTRY(hipEventElapsedTime(&ms, g->split_ev[2 * i], g->split_ev[2 * i + 1]));
+      g->split_ms[i] += ms;
+    }
+  } else {
+    if (g->slice_tiles) launch_slices(g, AS, 0, NSLICE * g->slice_tiles, s);
+    if (g->total_blocks) launch_rows(g, A, mode, 0, g->total_blocks, s);
   }
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
   if (!g->hubs.empty()) {
@@ -994,7 +1374,7 @@ int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s) {
   if (iterations == 0) {
     if (g->rank == 0 && n) hipLaunchKernelGGL(k_sources_one, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->outdeg, n, g->r_full);
   } else if (g->lrows) {
-    hipLaunchKernelGGL(k_scatter_ranks, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->perm, g->r_loc[iterations & 1], g->lrows, static_cast<uint32_t>(g->p), static_cast<uint32_t>(g->rank), g->r_full);
+    hipLaunchKernelGGL(k_scatter_ranks, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->perm, g->r_loc[iterations & 1], g->lrows, layout_of(g), g->r_full);
   }
   HIPTRY(hipGetLastError());
   return PR_OK;

@@ -1,8 +1,9 @@
 """World-size-2 CPU rehearsal (gloo) of the engine's multi-GPU protocol.
 
-The engine deals internal rows round-robin to ranks (rank j owns k = l*p + j), writes each
-rank's new contribution values into its own contiguous slot of x (A-row k at position
-(k % p)*maxA + k//p, C-vertex k at p*maxA + (k - R)), all-gathers the slots in place, and
+The engine deals internal rows to ranks in chunks of 16 (chunk c = k // 16 goes to rank
+c % p), writes each rank's new contribution values into its own contiguous slot of x
+(A-row k at owner(k)*maxA + local(k), C-vertex k at p*maxA + (k - R), maxA a multiple of
+16), all-gathers the slots in place, and
 sums the per-rank exact dangling records in any order.  This test replays that protocol
 with numpy on two gloo ranks and checks: (1) the assembled ranks are bit-identical to the
 same protocol at p = 1, (2) they match the oracle within 1e-9, (3) every edge and row is
@@ -37,17 +38,40 @@ def internal_order(src, dst, n, mapw):
 def protocol(rank, p, src, dst, n, mapw, n_tot, allgather, gather_records):
     perm, inv, (nA, nB, nC, _nD), outd, ind, dang_w = internal_order(src, dst, n, mapw)
     R = nA + nB
-    maxA = -(-nA // p)
-    X = p * maxA + nC
+    CH = 16
+
+    def owner(k):
+        return (k // CH) % p
+
+    def local(k):
+        return ((k // CH) // p) * CH + k % CH
+
+    # slice-major x (p divides 8): rank slot -> slice region (chunk % 8) -> chunk order
+    NS = 8
+    SL = CH * -(-(-(-nA // CH)) // NS)
+    SLC = CH * -(-(-(-nC // CH)) // NS)
+    maxA = (NS // p) * SL
+    X = p * maxA + NS * SLC
 
     def xpos(k):
-        return np.where(k < nA, (k % p) * maxA + k // p, p * maxA + (k - R))
+        c = k // CH
+        kc = k - R
+        cc = kc // CH
+        a = ((c % NS) % p) * maxA + ((c % NS) // p) * SL + (c // NS) * CH + k % CH
+        b = p * maxA + (cc % NS) * SLC + (cc // NS) * CH + kc % CH
+        return np.where(k < nA, a, b)
 
-    own = np.arange(rank, R, p)                            # internal rows of this rank
+    def xslot(l):                                           # local row -> offset in own slot
+        c = (l // CH) * p + rank
+        return ((c % NS) // p) * SL + (c // NS) * CH + l % CH
+
+    allrows = np.arange(R)
+    own = allrows[owner(allrows) == rank]                   # internal rows of this rank
+    assert np.array_equal(local(own), np.arange(len(own)))  # local rows are dense
     kd, ks = inv[dst], inv[src]
-    mine = (kd % p) == rank
-    order = np.lexsort((ks[mine], kd[mine] // p))          # (local row, internal source)
-    lrow = (kd[mine] // p)[order]
+    mine = owner(kd) == rank
+    order = np.lexsort((ks[mine], local(kd[mine])))        # (local row, internal source)
+    lrow = local(kd[mine])[order]
     lsrc = ks[mine][order]
     col = xpos(lsrc)
     rp = np.zeros(len(own) + 1, np.int64)
@@ -64,7 +88,8 @@ def protocol(rank, p, src, dst, n, mapw, n_tot, allgather, gather_records):
         r_loc = np.where(c > 0, 0.15 + (c + a) * 0.85, 0.0)
         slot = np.zeros(maxA)
         isA = own < nA
-        slot[np.nonzero(isA)[0]] = r_loc[isA] / outd[perm[own[isA]]]
+        slot[xslot(np.nonzero(isA)[0])] = r_loc[isA] / outd[perm[own[isA]]]
+        assert np.array_equal(rank * maxA + xslot(np.nonzero(isA)[0]), xpos(own[isA]))
         xn = np.zeros(X)
         xn[:p * maxA] = allgather(slot)                   # in-place all-gather of slots
         x = xn
