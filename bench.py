@@ -21,7 +21,9 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "page-rank-and-tfidf-using-apache-spark_amd"))
 
-import prmi355x as P  # noqa: E402  (load the engine before torch so it binds ROCm's own HIP)
+import prmi355x as P  # noqa: E402
+
+P.lib()  # load the engine (and ROCm's HIP + RCCL) before torch brings its own copies
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
