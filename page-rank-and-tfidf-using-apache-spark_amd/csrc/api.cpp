@@ -800,7 +800,7 @@ int pr_export_csr(pr_ctx* c, uint64_t* row_ptr, uint32_t* col, uint32_t* outdeg,
     // x positions -> internal ids (p = 1; inverse of the device layout)
     const uint32_t CH = prmi::CHUNK, NS = prmi::NSLICE;
     for (uint64_t e = 0; e < g.nnz; ++e) {
-      const uint32_t x = col[e] & 0x7FFFFFFFu;  // bit 31: cold-gather marker
+      const uint32_t x = col[e];
       if (!g.sm) {
         col[e] = x < g.maxA ? x : x - g.maxA + g.R;
       } else if (x < g.maxA) {

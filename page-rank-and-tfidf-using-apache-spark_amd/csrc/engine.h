@@ -70,8 +70,7 @@ struct Tuning {
   uint32_t seg = 4096;  // edges per hub segment
   uint32_t ks = 64;     // in-degree from which a row is XCD-sliced (PR_KS; huge = off)
   int nt = 0;           // non-temporal loads for the streamed CSR arrays
-  uint32_t hot = 0x7FFFFFFFu;  // PR_HOT: entries per slice region gathered with normal
-                               // loads; columns beyond are gathered non-temporally
+  uint32_t hot_lds = 20480;  // PR_HOTLDS: x entries of each slice region copied to LDS (<=20480)
   uint32_t colmask = 0xFFFFFFFFu;  // PR_COLMASK: timing-only gather working-set restriction
   int split = 0;        // PR_SPLIT: one launch per bin with events (timing breakdown only)
 };

@@ -179,6 +179,9 @@ struct StepArgs {
   uint32_t colmask;       // timing experiments only (PR_COLMASK); all-ones in production
   uint32_t block_base;    // first grid block of this launch (PR_SPLIT timing mode)
   uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
+  uint32_t tile_end;         // slice launch: one past the last wave-tile of this launch
+  uint32_t hot_n;            // slice launch: x entries per slice cached in LDS
+  uint32_t hot_base[NSLICE]; // slice launch: x position of each slice region's start
 };
 
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
@@ -205,22 +208,29 @@ __device__ __forceinline__ T ld_stream(const T* p) {
   else return *p;
 }
 
+// Gathers of x: plain loads, or -- in the persistent slice kernel -- the first H entries of
+// the slice's region (its hottest sources) served from an LDS copy.
+struct GatherX {
+  const double* __restrict__ x;
+  uint32_t cm;  // PR_COLMASK (timing experiments only)
+  __device__ __forceinline__ double operator()(uint32_t q) const { return x[q & cm]; }
+};
+struct GatherLds {
+  const double* __restrict__ x;
+  const double* lds;
+  uint32_t base, H, cm;
+  __device__ __forceinline__ double operator()(uint32_t q) const {
+    q &= cm;
+    const uint32_t o = q - base;
+    return o < H ? lds[o] : x[q];
+  }
+};
+
 // Partial sum of x[col[e]] over e = beg + lane, beg + lane + S, ... < end, with four
 // independent gathers in flight per lane.  Fixed order: depends on (end-beg, S) only.
-// Gather of x[c]; bit 31 of a column index marks a cold entry (beyond the L2-resident
-// prefix of its slice): it is loaded non-temporally so it does not evict hot lines.
-template <int NT>
-__device__ __forceinline__ double gather_x(const double* __restrict__ x, uint32_t raw,
-                                           uint32_t cm) {
-  const uint32_t c = raw & 0x7FFFFFFFu & cm;
-  if (raw >> 31) return __builtin_nontemporal_load(x + c);
-  return x[c];
-}
-
-template <int S, int NT>
-__device__ __forceinline__ double strided_sum(const uint32_t* __restrict__ col,
-                                              const double* __restrict__ x, uint64_t beg,
-                                              uint64_t end, int lane, uint32_t cm) {
+template <int S, int NT, class Gx>
+__device__ __forceinline__ double strided_sum(const uint32_t* __restrict__ col, const Gx& gx,
+                                              uint64_t beg, uint64_t end, int lane) {
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   for (uint64_t e = beg + lane; e < end; e += 4ull * S) {
     const uint64_t e1 = e + S, e2 = e + 2ull * S, e3 = e + 3ull * S;
@@ -228,10 +238,10 @@ __device__ __forceinline__ double strided_sum(const uint32_t* __restrict__ col,
     const uint32_t c1 = e1 < end ? ld_stream<NT>(col + e1) : 0u;
     const uint32_t c2 = e2 < end ? ld_stream<NT>(col + e2) : 0u;
     const uint32_t c3 = e3 < end ? ld_stream<NT>(col + e3) : 0u;
-    const double v0 = gather_x<NT>(x, c0, cm);
-    const double v1 = e1 < end ? gather_x<NT>(x, c1, cm) : 0.0;
-    const double v2 = e2 < end ? gather_x<NT>(x, c2, cm) : 0.0;
-    const double v3 = e3 < end ? gather_x<NT>(x, c3, cm) : 0.0;
+    const double v0 = gx(c0);
+    const double v1 = e1 < end ? gx(c1) : 0.0;
+    const double v2 = e2 < end ? gx(c2) : 0.0;
+    const double v3 = e3 < end ? gx(c3) : 0.0;
     s0 += v0;
     s1 += v1;
     s2 += v2;
@@ -309,8 +319,8 @@ __device__ __forceinline__ void group_tile(const StepArgs& A, double a, const Bi
   const bool active = row < b.row_end;
   double s = 0.0;
   if (active)
-    s = strided_sum<G, NT>(A.col, A.x_in, ld_stream<NT>(A.row_ptr + row),
-                           ld_stream<NT>(A.row_ptr + row + 1), gl, A.colmask);
+    s = strided_sum<G, NT>(A.col, GatherX{A.x_in, A.colmask}, ld_stream<NT>(A.row_ptr + row),
+                           ld_stream<NT>(A.row_ptr + row + 1), gl);
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
   row_epilogue<MODE>(A, a, b.cls, row, s, active && gl == 0, lds);
@@ -352,16 +362,16 @@ __global__ __launch_bounds__(BLOCK) void spmv_round(StepArgs A) {
     case KIND_COMBINE: combine_tile<MODE>(A, a, bin, blk, lds); break;
     case KIND_BLOCK: {
       const uint32_t row = bin.row_begin + blk;
-      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, A.row_ptr[row], A.row_ptr[row + 1],
-                                        threadIdx.x, A.colmask);
+      double s = strided_sum<BLOCK, NT>(A.col, GatherX{A.x_in, A.colmask}, A.row_ptr[row],
+                                        A.row_ptr[row + 1], threadIdx.x);
       s = block_sum(s, red);
       row_epilogue<MODE>(A, a, bin.cls, row, s, threadIdx.x == 0, lds);
       break;
     }
     default: {  // KIND_HUB: one segment of an unsliced split row (combined in hub_round)
       const HubSeg seg = A.segs[bin.seg_begin + blk];
-      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, seg.e_begin, seg.e_end, threadIdx.x,
-                                        A.colmask);
+      double s = strided_sum<BLOCK, NT>(A.col, GatherX{A.x_in, A.colmask}, seg.e_begin,
+                                        seg.e_end, threadIdx.x);
       s = block_sum(s, red);
       if (threadIdx.x == 0) A.hub_part[seg.part] = s;
       break;
@@ -369,14 +379,25 @@ __global__ __launch_bounds__(BLOCK) void spmv_round(StepArgs A) {
   }
 }
 
-// ---- the slice launch: grid = 8 x tiles, slice j = blockIdx % 8 (one XCD per slice) ----
-template <int G, int NT>
-__device__ __forceinline__ void slice_group(const StepArgs& A, const Bin& b, uint32_t blk,
-                                            uint32_t j) {
-  constexpr uint32_t RPB = BLOCK / G;
-  const uint32_t i = blk * RPB + threadIdx.x / G;
+// ---- the slice launch: persistent, slice j = blockIdx % 8 (one XCD per slice) ----------
+// Every wave walks the wave-tiles of its slice with a static stride; a tile is 64/G rows of
+// a grouped bin, one (row, slice) sub-list of a long row, or one hub segment.  The first H
+// entries of the slice's x region (its hottest sources) are copied to LDS once per round.
+constexpr int SLICE_BLOCK = 1024;
+
+__device__ __forceinline__ double wave_sum(double s) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  return s;
+}
+
+template <int G, int NT, class Gx>
+__device__ __forceinline__ void slice_group(const StepArgs& A, const Gx& gx, const Bin& b,
+                                            uint32_t tile, uint32_t j, int lane) {
+  constexpr uint32_t RPW = 64 / G;
+  const uint32_t i = tile * RPW + lane / G;
   const uint32_t row = b.row_begin + i;
-  const int gl = threadIdx.x % G;
+  const int gl = lane % G;
   const bool active = row < b.row_end;
   double s = 0.0;
   const uint32_t sr = b.srow_begin + i;
@@ -384,47 +405,61 @@ __device__ __forceinline__ void slice_group(const StepArgs& A, const Bin& b, uin
     const uint64_t base = ld_stream<NT>(A.row_ptr + row);
     const uint64_t beg = base + ld_stream<NT>(A.sb + static_cast<uint64_t>(j) * A.nS + sr);
     const uint64_t end = base + ld_stream<NT>(A.sb + static_cast<uint64_t>(j + 1) * A.nS + sr);
-    s = strided_sum<G, NT>(A.col, A.x_in, beg, end, gl, A.colmask);
+    s = strided_sum<G, NT>(A.col, gx, beg, end, gl);
   }
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
   if (active && gl == 0) A.part[static_cast<uint64_t>(j) * A.nS + sr] = s;
 }
 
-template <int NT>
-__global__ __launch_bounds__(BLOCK) void spmv_slices(StepArgs A) {
-  __shared__ double red[4];
-  const uint32_t b = blockIdx.x + A.block_base;
-  const uint32_t j = b % NSLICE, t = b / NSLICE;
+template <int NT, class Gx>
+__device__ __forceinline__ void slice_tile(const StepArgs& A, const Gx& gx, uint32_t t,
+                                           uint32_t j, int lane) {
   const Bin bin = A.bins[find_bin(A.bins, A.nbins, t)];
-  const uint32_t blk = t - bin.block_begin;
+  const uint32_t tt = t - bin.block_begin;
   switch (bin.kind) {
-    case 0: slice_group<1, NT>(A, bin, blk, j); break;
-    case 1: slice_group<2, NT>(A, bin, blk, j); break;
-    case 2: slice_group<4, NT>(A, bin, blk, j); break;
-    case 3: slice_group<8, NT>(A, bin, blk, j); break;
-    case 4: slice_group<16, NT>(A, bin, blk, j); break;
-    case 5: slice_group<32, NT>(A, bin, blk, j); break;
-    case 6: slice_group<64, NT>(A, bin, blk, j); break;
-    case KIND_BLOCK: {
-      const uint32_t row = bin.row_begin + blk;
-      const uint32_t sr = bin.srow_begin + blk;
+    case 0: slice_group<1, NT>(A, gx, bin, tt, j, lane); break;
+    case 1: slice_group<2, NT>(A, gx, bin, tt, j, lane); break;
+    case 2: slice_group<4, NT>(A, gx, bin, tt, j, lane); break;
+    case 3: slice_group<8, NT>(A, gx, bin, tt, j, lane); break;
+    case 4: slice_group<16, NT>(A, gx, bin, tt, j, lane); break;
+    case 5: slice_group<32, NT>(A, gx, bin, tt, j, lane); break;
+    case 6: slice_group<64, NT>(A, gx, bin, tt, j, lane); break;
+    case KIND_BLOCK: {  // one long (row, slice) sub-list per wave
+      const uint32_t row = bin.row_begin + tt;
+      const uint32_t sr = bin.srow_begin + tt;
       const uint64_t base = A.row_ptr[row];
       const uint64_t beg = base + A.sb[static_cast<uint64_t>(j) * A.nS + sr];
       const uint64_t end = base + A.sb[static_cast<uint64_t>(j + 1) * A.nS + sr];
-      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, beg, end, threadIdx.x, A.colmask);
-      s = block_sum(s, red);
-      if (threadIdx.x == 0) A.part[static_cast<uint64_t>(j) * A.nS + sr] = s;
+      const double s = wave_sum(strided_sum<64, NT>(A.col, gx, beg, end, lane));
+      if (lane == 0) A.part[static_cast<uint64_t>(j) * A.nS + sr] = s;
       break;
     }
     default: {  // KIND_HUB: slice j's segment list (padded with empty segments)
-      const HubSeg seg = A.segs[static_cast<uint64_t>(j) * A.hub_tiles + bin.seg_begin + blk];
-      double s = strided_sum<BLOCK, NT>(A.col, A.x_in, seg.e_begin, seg.e_end, threadIdx.x,
-                                        A.colmask);
-      s = block_sum(s, red);
-      if (threadIdx.x == 0 && seg.part != 0xFFFFFFFFu) A.hub_part[seg.part] = s;
+      const HubSeg seg = A.segs[static_cast<uint64_t>(j) * A.hub_tiles + bin.seg_begin + tt];
+      const double s = wave_sum(strided_sum<64, NT>(A.col, gx, seg.e_begin, seg.e_end, lane));
+      if (lane == 0 && seg.part != 0xFFFFFFFFu) A.hub_part[seg.part] = s;
       break;
     }
+  }
+}
+
+template <int NT, bool HOT>
+__global__ __launch_bounds__(SLICE_BLOCK) void spmv_slices(StepArgs A) {
+  extern __shared__ __attribute__((aligned(16))) double hot[];
+  const uint32_t j = blockIdx.x % NSLICE, bi = blockIdx.x / NSLICE;
+  const uint32_t nb = gridDim.x / NSLICE, nw = blockDim.x / 64;
+  const int lane = threadIdx.x & 63;
+  const uint32_t w0 = bi * nw + threadIdx.x / 64, stride = nb * nw;
+  if constexpr (HOT) {
+    const uint32_t base = A.hot_base[j], H = A.hot_n;
+    for (uint32_t i = threadIdx.x; i < H; i += blockDim.x) hot[i] = A.x_in[base + i];
+    __syncthreads();
+    const GatherLds gx{A.x_in, hot, base, H, A.colmask};
+    for (uint32_t t = A.block_base + w0; t < A.tile_end; t += stride) slice_tile<NT>(A, gx, t, j, lane);
+  } else {
+    const GatherX gx{A.x_in, A.colmask};
+    for (uint32_t t = A.block_base + w0; t < A.tile_end; t += stride) slice_tile<NT>(A, gx, t, j, lane);
   }
 }
 
@@ -696,14 +731,11 @@ __device__ __forceinline__ int srow_of(const SliceRows& S, uint32_t l) {
 
 // col = x position of the source; per (sliced row, slice) edge counts
 __global__ void k_col(const uint64_t* lk, uint64_t lnnz, int nb, Layout L, SliceRows S,
-                      uint32_t hot, uint32_t* col, uint32_t* cnt) {
+                      uint32_t* col, uint32_t* cnt) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   if (e >= lnnz) return;
   const uint64_t key = lk[e];
-  const uint32_t ksrc = static_cast<uint32_t>(key & ((1ull << nb) - 1));
-  // cold = beyond the first `hot` entries of the source's slice region (slice-major only)
-  const bool cold = L.sm && (ksrc >= L.nA || (ksrc / CHUNK) / NSLICE * CHUNK >= hot);
-  col[e] = xpos(L, ksrc) | (cold ? 0x80000000u : 0u);
+  col[e] = xpos(L, static_cast<uint32_t>(key & ((1ull << nb) - 1)));
   const int sr = srow_of(S, static_cast<uint32_t>(key >> (nb + 3)));
   if (sr >= 0) {
     const uint32_t sl = static_cast<uint32_t>((key >> nb) & 7);
@@ -848,7 +880,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.seg = static_cast<uint32_t>(std::max(256, env_int("PR_SEG", static_cast<int>(T.seg))));
   T.ks = static_cast<uint32_t>(std::max(1, env_int("PR_KS", static_cast<int>(T.ks))));
   T.nt = env_int("PR_NT", T.nt);
-  T.hot = static_cast<uint32_t>(env_int("PR_HOT", static_cast<int>(T.hot)));
+  T.hot_lds = static_cast<uint32_t>(std::max(0, std::min(20480, env_int("PR_HOTLDS", static_cast<int>(T.hot_lds)))));
   T.split = env_int("PR_SPLIT", 0);
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   const uint32_t n = in.n;
@@ -1067,7 +1099,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   uint32_t* cnt = nullptr;
   TRY(dmalloc(&cnt, static_cast<size_t>(NSLICE) * g->nS, err));
   if (g->nS) HIPTRY(hipMemsetAsync(cnt, 0, 4ull * NSLICE * g->nS, s));
-  if (lnnz) hipLaunchKernelGGL(k_col, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk_sorted, lnnz, nb, L, SR, T.hot, g->col, cnt);
+  if (lnnz) hipLaunchKernelGGL(k_col, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk_sorted, lnnz, nb, L, SR, g->col, cnt);
   TRY(dmalloc(&g->sb, (NSLICE + 1ull) * g->nS, err));
   if (g->nS) hipLaunchKernelGGL(k_slice_prefix, dim3(grid_for(g->nS)), dim3(BLOCK), 0, s, cnt, g->nS, g->sb);
   HIPTRY(hipStreamSynchronize(s));
@@ -1145,7 +1177,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
         b.cls = static_cast<uint16_t>(cls);
         b.srow_begin = srow0 + i;
         const uint32_t rows = e - i;
-        tiles += kd == KIND_BLOCK ? rows : (rows + (BLOCK >> kd) - 1) / (BLOCK >> kd);
+        tiles += kd == KIND_BLOCK ? rows : (rows + (64u >> kd) - 1) / (64u >> kd);
         g->sbins.push_back(b);
         g->sbin_edges.push_back(hrow[r0 + e] - hrow[r0 + i]);
         i = e;
@@ -1273,10 +1305,29 @@ void launch_rows(const DevGraph* g, StepArgs A, int mode, uint32_t base, uint32_
     else hipLaunchKernelGGL((spmv_round<2, 0>), gr, bl, 0, s, A);
   }
 }
-void launch_slices(const DevGraph* g, StepArgs A, uint32_t base, uint32_t nblk, hipStream_t s) {
-  A.block_base = base;
-  if (g->tune.nt) hipLaunchKernelGGL((spmv_slices<1>), dim3(nblk), dim3(BLOCK), 0, s, A);
-  else hipLaunchKernelGGL((spmv_slices<0>), dim3(nblk), dim3(BLOCK), 0, s, A);
+void launch_slices(const DevGraph* g, StepArgs A, uint32_t t0, uint32_t t1, hipStream_t s) {
+  A.block_base = t0;
+  A.tile_end = t1;
+  const bool hot = A.hot_n > 0;
+  const size_t lds = hot ? 8ull * A.hot_n : 0;
+  // persistent grid: 32 CUs per XCD; one 1024-thread block per CU with the LDS copy of the
+  // hot x prefix, two without it
+  const dim3 gr(NSLICE * 32 * (hot ? 1 : 2)), bl(SLICE_BLOCK);
+  static bool attr_set = false;  // allow the >64 KB dynamic LDS request
+  if (hot && !attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_slices<0, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_slices<1, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  if (g->tune.nt) {
+    if (hot) hipLaunchKernelGGL((spmv_slices<1, true>), gr, bl, lds, s, A);
+    else hipLaunchKernelGGL((spmv_slices<1, false>), gr, bl, 0, s, A);
+  } else {
+    if (hot) hipLaunchKernelGGL((spmv_slices<0, true>), gr, bl, lds, s, A);
+    else hipLaunchKernelGGL((spmv_slices<0, false>), gr, bl, 0, s, A);
+  }
 }
 
 }  // namespace
@@ -1305,6 +1356,9 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.rank = static_cast<uint32_t>(g->rank);
   A.sm = g->sm ? 1u : 0u;
   A.SL = g->SL;
+  A.hot_n = g->sm ? std::min(g->tune.hot_lds, g->SL) : 0u;
+  for (int j = 0; j < NSLICE; ++j)
+    A.hot_base[j] = g->sm ? (j % g->p) * g->maxA + (j / g->p) * g->SL : 0u;
   StepArgs AS = A;  // slice launch
   AS.bins = g->d_sbins;
   AS.nbins = static_cast<int>(g->sbins.size());
@@ -1330,7 +1384,7 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
       const uint32_t b1 = k + 1 < bv.size() ? bv[k + 1].block_begin : tot;
       HIPTRY(hipEventRecord(g->split_ev[2 * i], s));
       if (b1 > b0) {
-        if (sl) launch_slices(g, AS, NSLICE * b0, NSLICE * (b1 - b0), s);
+        if (sl) launch_slices(g, AS, b0, b1, s);
         else launch_rows(g, A, mode, b0, b1 - b0, s);
       }
       HIPTRY(hipEventRecord(g->split_ev[2 * i + 1], s));
@@ -1342,7 +1396,7 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
       g->split_ms[i] += ms;
     }
   } else {
-    if (g->slice_tiles) launch_slices(g, AS, 0, NSLICE * g->slice_tiles, s);
+    if (g->slice_tiles) launch_slices(g, AS, 0, g->slice_tiles, s);
     if (g->total_blocks) launch_rows(g, A, mode, 0, g->total_blocks, s);
   }
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
