@@ -90,10 +90,11 @@ int build_device(pr_ctx* c, const prmi::BuildInput& in) {
   c->last_iters = -1;
   c->host_ranks_valid = false;
   if (c->opts.flags & PR_F_VERBOSE)
-    fprintf(stderr, "[prmi355x] rank %d build %.1f ms: n=%u nnz=%llu rows=%u local_rows=%u local_nnz=%llu bins=%zu hubs=%zu blocks=%u\n",
+    fprintf(stderr, "[prmi355x] rank %d build %.1f ms: n=%u nnz=%llu rows=%u local_rows=%u local_nnz=%llu segments/slice=%u pairs=%llu pieces=%llu tasks=%u row_bins=%zu row_blocks=%u\n",
             c->opts.rank, c->dg.ms_build, c->dg.n, (unsigned long long)c->dg.nnz, c->dg.R,
-            c->dg.lrows, (unsigned long long)c->dg.lnnz, c->dg.bins.size(), c->dg.hubs.size(),
-            c->dg.total_blocks);
+            c->dg.lrows, (unsigned long long)c->dg.lnnz, c->dg.nseg,
+            (unsigned long long)c->dg.n_pairs, (unsigned long long)c->dg.n_pieces,
+            c->dg.tbase[prmi::NSLICE], c->dg.bins.size(), c->dg.total_blocks);
   return PR_OK;
 }
 
@@ -640,19 +641,6 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   }
   c->last_iters = done;
   if (st) *st = s;
-  if (!g->split_ms.empty()) {  // PR_SPLIT timing breakdown (per bin, summed over rounds)
-    const size_t nsb = g->sbins.size();
-    for (size_t i = 0; i < g->split_ms.size(); ++i) {
-      const bool sl = i < nsb;
-      const prmi::Bin& b = sl ? g->sbins[i] : g->bins[i - nsb];
-      const uint64_t edges = sl ? g->sbin_edges[i] : g->bin_edges[i - nsb];
-      const double ms = g->split_ms[i] / done;
-      fprintf(stderr, "[prmi355x] %s bin %2zu kind %u cls %u rows %9u edges %11llu  %8.3f ms/round  %6.1f GTEPS\n",
-              sl ? "slice" : "row  ", sl ? i : i - nsb, b.kind, b.cls, b.row_end - b.row_begin,
-              (unsigned long long)edges, ms, ms > 0 ? edges / (ms * 1e6) : 0.0);
-    }
-    std::fill(g->split_ms.begin(), g->split_ms.end(), 0.0);
-  }
   return PR_OK;
 }
 
@@ -789,29 +777,14 @@ int pr_export_csr(pr_ctx* c, uint64_t* row_ptr, uint32_t* col, uint32_t* outdeg,
     HIPCHK(c, hipMemcpyAsync(od.data(), g.outdeg, 4ull * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(dw.data(), g.dang_w, 4ull * n, hipMemcpyDeviceToHost, c->stream));
   }
-  if (row_ptr) {
-    HIPCHK(c, hipMemcpyAsync(row_ptr, g.row_ptr, 8ull * (g.lrows + 1), hipMemcpyDeviceToHost, c->stream));
+  if (row_ptr || col) {
+    std::string e;
+    rc = prmi::dev_export_csr(&c->dg, row_ptr, col, c->stream, &e);
+    if (rc) return fail(c, rc, "export csr: " + e);
   }
-  if (col && g.nnz) HIPCHK(c, hipMemcpyAsync(col, g.col, 4ull * g.nnz, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (row_ptr)
     for (uint64_t k = g.lrows + 1ull; k <= n; ++k) row_ptr[k] = g.nnz;
-  if (col) {
-    // x positions -> internal ids (p = 1; inverse of the device layout)
-    const uint32_t CH = prmi::CHUNK, NS = prmi::NSLICE;
-    for (uint64_t e = 0; e < g.nnz; ++e) {
-      const uint32_t x = col[e];
-      if (!g.sm) {
-        col[e] = x < g.maxA ? x : x - g.maxA + g.R;
-      } else if (x < g.maxA) {
-        const uint32_t sl = x / g.SL, r = x % g.SL;
-        col[e] = ((r / CH) * NS + sl) * CH + r % CH;
-      } else {
-        const uint32_t q = x - g.maxA, sl = q / g.SLC, r = q % g.SLC;
-        col[e] = g.R + ((r / CH) * NS + sl) * CH + r % CH;
-      }
-    }
-  }
   for (uint32_t k = 0; k < n; ++k) {
     if (outdeg) outdeg[k] = od[perm[k]];
     if (dang_w) dang_w[k] = dw[perm[k]];

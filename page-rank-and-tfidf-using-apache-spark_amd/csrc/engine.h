@@ -8,10 +8,15 @@
 //     class D [R+nC,n)      in==0, out==0   neither
 //   rows k < R are dealt to ranks in chunks of 16: chunk c = k>>4 goes to rank c % p
 //   XCD slicing: the columns of x are cut into 8 slices by 128-byte chunk (slice = chunk
-//   index mod 8); the edges of a row with in-degree >= ks are grouped by slice, and slice
-//   j's partial sums are computed only by workgroups with blockIdx % 8 == j (one XCD), so
-//   each XCD's L2 caches 1/8 of x.  x is stored slice-major (p divides 8): rank slot, then
-//   slice region, then chunks in hotness order -- each slice is one contiguous range.
+//   index mod 8).  Slice j's edges form ONE stream that only workgroups with
+//   blockIdx % 8 == j (one XCD) read, so each XCD's L2 caches 1/8 of x.  Inside a slice the
+//   columns are in hotness order (position q); the stream is ordered by (segment of q,
+//   local row, q): segment 0 = the hot prefix [0, QH) (its first H entries served from an
+//   LDS copy), then cold segments of S entries each, so a cold segment's x lines are
+//   fetched once and reused from L2 while the XCD sweeps it.
+//   A "pair" = the edges of one (row, slice, segment); a "piece" = a pair cut at the
+//   1024-edge task boundaries of the stream.  The stream kernel writes one partial sum per
+//   piece; the row kernel adds a row's pieces (row-major piece list) in a fixed order.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -32,25 +37,16 @@ constexpr int BLOCK = 256;
 constexpr int NSLICE = 8;          // one slice per XCD
 constexpr int CHUNK = 16;          // rows dealt per rank chunk = entries per 128-B x line
 
-// kinds 0..6: 2^kind lanes per row; then one workgroup per row; hub segment; combine
-enum : uint16_t { KIND_BLOCK = 7, KIND_HUB = 8, KIND_COMBINE = 9 };
+constexpr int EPL = 16;            // stream edges per lane per task
+constexpr int TASK = 64 * EPL;     // stream edges per wave task (1024)
+
+// row-kernel kinds 0..6: 2^kind lanes per row; then one workgroup per row
+enum : uint16_t { KIND_BLOCK = 7 };
 
 struct Bin {
-  uint32_t block_begin;  // first tile of this bin in its launch's grid
+  uint32_t block_begin;  // first tile of this bin in the row launch's grid
   uint32_t row_begin, row_end;
-  uint32_t seg_begin;    // hub bins: first segment (tile) index
   uint16_t kind, cls;    // cls 0 = class A rows, 1 = class B rows
-  uint32_t srow_begin;   // sliced rows: slice-row index of row_begin
-};
-
-struct HubSeg {
-  uint64_t e_begin, e_end;
-  uint32_t part;         // hub_part slot (UINT32_MAX: padding, nothing to write)
-  uint32_t pad;
-};
-
-struct HubRow {
-  uint32_t row, part_begin, part_end, cls;
 };
 
 struct IterState {
@@ -64,15 +60,15 @@ struct IterState {
 };
 
 struct Tuning {
-  int epl = 4;          // target edges per lane for the grouped bins
-  uint32_t kb = 1024;   // (sub-)row length above which one workgroup takes a row
-  uint32_t kh = 16384;  // in-degree above which a row is split into segments
-  uint32_t seg = 4096;  // edges per hub segment
-  uint32_t ks = 64;     // in-degree from which a row is XCD-sliced (PR_KS; huge = off)
-  int nt = 0;           // non-temporal loads for the streamed CSR arrays
+  int epl = 4;          // row kernel: target pieces per lane
+  uint32_t kb = 1024;   // row kernel: piece count above which one workgroup takes a row
+  uint32_t qh = 458752; // PR_QH: hot segment length per slice (x entries, 3.5 MiB)
+  uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
+  int nt = 1;           // PR_NT: non-temporal loads for the streamed arrays
   uint32_t hot_lds = 20480;  // PR_HOTLDS: x entries of each slice region copied to LDS (<=20480)
   uint32_t colmask = 0xFFFFFFFFu;  // PR_COLMASK: timing-only gather working-set restriction
-  int split = 0;        // PR_SPLIT: one launch per bin with events (timing breakdown only)
+  int dbg = 0;          // PR_DBG: timing-only experiments in the stream kernel (see StreamArgs)
+  int stream_wg = 1;    // PR_STREAM_WG: stream workgroups per CU (1 with the LDS copy)
 };
 
 struct DevGraph {
@@ -91,18 +87,24 @@ struct DevGraph {
   uint64_t n_dang_entries = 0;
   uint64_t digest[2] = {0, 0};
   double ms_build = 0;
-  // sliced rows: class A [0,sA), class B [lA,lA+sB); hubs lead each range (hA, hB)
-  uint32_t sA = 0, sB = 0, hA = 0, hB = 0, nS = 0;
+  // slice streams: slice j's edges at [sbase[j], sbase[j] + slen[j]) of col / bits
+  uint64_t sbase[NSLICE] = {}, slen[NSLICE] = {};
+  uint32_t tbase[NSLICE + 1] = {};  // first global task of slice j (tbase[8] = all tasks)
+  uint32_t nseg = 0;              // segments per slice (hot + cold)
+  uint64_t n_pieces = 0, n_pairs = 0;
+  uint64_t stream_len = 0;        // padded length of col (multiple of TASK)
   // device arrays
-  uint64_t* row_ptr = nullptr;
-  uint32_t* col = nullptr;
+  uint32_t* col = nullptr;        // [stream_len] x position of each stream edge
+  uint16_t* bits = nullptr;       // [stream_len/16] pair-start flags
+  uint32_t* task_piece = nullptr; // [tasks+1] first piece of each task
+  double* partial = nullptr;      // [n_pieces] per-piece partial sums
+  uint32_t* row_pp = nullptr;     // [lrows+1] offsets into pidx
+  uint32_t* pidx = nullptr;       // [n_pieces] pieces of each row, stream order
   uint32_t* meta = nullptr;
   uint32_t* perm = nullptr;       // internal -> original
   uint32_t* outdeg = nullptr;     // by original id
   uint32_t* indeg = nullptr;
   uint32_t* dang_w = nullptr;
-  uint32_t* sb = nullptr;         // [9][nS] slice offsets inside each sliced row
-  double* part = nullptr;         // [8][nS] per-slice partial row sums
   double* x_init = nullptr;
   double* xbuf[2] = {nullptr, nullptr};
   double* r_loc[2] = {nullptr, nullptr};
@@ -111,26 +113,11 @@ struct DevGraph {
   uint64_t* rec_local = nullptr;  // [REC_WORDS]
   uint64_t* rec_all = nullptr;    // [p][REC_WORDS]
   IterState* state = nullptr;
-  // schedule: the row launch (light rows + combine + unsliced hubs) ...
+  // row launch schedule
   std::vector<Bin> bins;
-  std::vector<uint64_t> bin_edges;
   Bin* d_bins = nullptr;
   uint32_t total_blocks = 0;
-  HubSeg* d_segs = nullptr;       // unsliced hub segments
-  // ... and the slice launch (grid = 8 x slice_tiles)
-  std::vector<Bin> sbins;
-  std::vector<uint64_t> sbin_edges;
-  Bin* d_sbins = nullptr;
-  uint32_t slice_tiles = 0;
-  HubSeg* d_ssegs = nullptr;      // [8][hub tiles] sliced hub segments (padded)
-  uint32_t hub_tiles = 0;
-  std::vector<HubRow> hubs;
-  HubRow* d_hubs = nullptr;
-  double* hub_part = nullptr;
-  uint32_t n_parts = 0;
   Tuning tune;
-  std::vector<hipEvent_t> split_ev;  // PR_SPLIT timing mode
-  std::vector<double> split_ms;
 };
 
 struct BuildInput {
@@ -164,6 +151,8 @@ double* dev_x_out(DevGraph* g, int t);
 // Scatter this rank's final ranks into r_full (by original id; zeros elsewhere).
 // iterations == 0 reproduces ranks = 1.0 on sources (PageRank.java:76-83).
 int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s);
+// Host copy of this rank's pull CSR (single-rank graphs: internal ids, sources ascending).
+int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s, std::string* err);
 // Internal id of this rank's local row l (host copy of the device mapping).
 inline uint32_t row_internal(const DevGraph* g, uint32_t l) {
   return (((l / CHUNK) * static_cast<uint32_t>(g->p) + static_cast<uint32_t>(g->rank)) * CHUNK) +

@@ -155,37 +155,27 @@ __device__ double sa_to_double_dev(const uint64_t* limb) {
 }
 
 // =======================================================================================
-// the round: XCD-sliced partial sums + fused row launch (combine / light rows / epilogue)
+// the round: slice streams (per-piece partial sums) + fused row launch (combine + epilogue)
 // =======================================================================================
-struct StepArgs {
+// Row launch: a row's value c = fixed-order sum of its pieces' partials, then PageRank.java's
+// damping / contribution epilogue.
+struct RowArgs {
   const Bin* bins;
   int nbins;
-  const uint64_t* row_ptr;
-  const uint32_t* col;
+  const uint32_t* row_pp;  // [lrows+1] offsets into pidx
+  const uint32_t* pidx;    // pieces of each row (stream order)
+  const double* partial;   // per-piece partial sums of this round
   const uint32_t* meta;
-  const double* x_in;
-  double* x_out;          // this rank's slot of the next x
-  const double* r_old;    // tracked mode: previous ranks (nullptr = r^0 == 1)
+  double* x_out;           // this rank's slot of the next x
+  const double* r_old;     // tracked mode: previous ranks (nullptr = r^0 == 1)
   double* r_out;
-  const HubSeg* segs;     // hub segments of this launch
-  double* hub_part;
-  const HubRow* hubs;
   const IterState* st;
   uint64_t* shards;
-  const uint32_t* sb;     // [9][nS] slice offsets of sliced rows
-  double* part;           // [8][nS] slice partials
-  uint32_t nS;
-  uint32_t hub_tiles;     // per-slice stride of the sliced hub segment table
-  uint32_t colmask;       // timing experiments only (PR_COLMASK); all-ones in production
-  uint32_t block_base;    // first grid block of this launch (PR_SPLIT timing mode)
   uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
-  uint32_t tile_end;         // slice launch: one past the last wave-tile of this launch
-  uint32_t hot_n;            // slice launch: x entries per slice cached in LDS
-  uint32_t hot_base[NSLICE]; // slice launch: x position of each slice region's start
 };
 
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
-__device__ __forceinline__ uint32_t xslot_of(const StepArgs& A, uint32_t l) {
+__device__ __forceinline__ uint32_t xslot_of(const RowArgs& A, uint32_t l) {
   if (!A.sm) return l;
   const uint32_t c = (l / CHUNK) * A.p + A.rank, sl = c % NSLICE;
   return (sl / A.p) * A.SL + (c / NSLICE) * CHUNK + (l % CHUNK);
@@ -208,22 +198,9 @@ __device__ __forceinline__ T ld_stream(const T* p) {
   else return *p;
 }
 
-// Gathers of x: plain loads, or -- in the persistent slice kernel -- the first H entries of
-// the slice's region (its hottest sources) served from an LDS copy.
 struct GatherX {
   const double* __restrict__ x;
-  uint32_t cm;  // PR_COLMASK (timing experiments only)
-  __device__ __forceinline__ double operator()(uint32_t q) const { return x[q & cm]; }
-};
-struct GatherLds {
-  const double* __restrict__ x;
-  const double* lds;
-  uint32_t base, H, cm;
-  __device__ __forceinline__ double operator()(uint32_t q) const {
-    q &= cm;
-    const uint32_t o = q - base;
-    return o < H ? lds[o] : x[q];
-  }
+  __device__ __forceinline__ double operator()(uint32_t q) const { return x[q]; }
 };
 
 // Partial sum of x[col[e]] over e = beg + lane, beg + lane + S, ... < end, with four
@@ -262,7 +239,7 @@ __device__ __forceinline__ double block_sum(double s, double* red) {
 // Epilogue for one row per group leader, then the block's exact partials (dangling mass +
 // count for class-B rows; residual + rank sum in tracked mode) into the atomic shards.
 template <int MODE>
-__device__ __forceinline__ void row_epilogue(const StepArgs& A, double a, uint32_t cls,
+__device__ __forceinline__ void row_epilogue(const RowArgs& A, double a, uint32_t cls,
                                              uint32_t row, double c, bool leader,
                                              uint64_t (*lds)[REC_WORDS]) {
   double r = 0.0;
@@ -309,9 +286,10 @@ __device__ __forceinline__ void row_epilogue(const StepArgs& A, double a, uint32
   }
 }
 
-// G lanes per row (G <= 64): a workgroup takes 256/G consecutive rows of one bin.
-template <int G, int MODE, int NT>
-__device__ __forceinline__ void group_tile(const StepArgs& A, double a, const Bin& b,
+// G lanes per row (G <= 64): a workgroup takes 256/G consecutive rows of one bin; the row's
+// pieces are summed with strided_sum (shape fixed by the piece count and G).
+template <int G, int MODE>
+__device__ __forceinline__ void group_tile(const RowArgs& A, double a, const Bin& b,
                                            uint32_t blk, uint64_t (*lds)[REC_WORDS]) {
   constexpr uint32_t RPB = BLOCK / G;
   const uint32_t row = b.row_begin + blk * RPB + threadIdx.x / G;
@@ -319,160 +297,189 @@ __device__ __forceinline__ void group_tile(const StepArgs& A, double a, const Bi
   const bool active = row < b.row_end;
   double s = 0.0;
   if (active)
-    s = strided_sum<G, NT>(A.col, GatherX{A.x_in, A.colmask}, ld_stream<NT>(A.row_ptr + row),
-                           ld_stream<NT>(A.row_ptr + row + 1), gl);
+    s = strided_sum<G, 1>(A.pidx, GatherX{A.partial}, A.row_pp[row], A.row_pp[row + 1], gl);
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
   row_epilogue<MODE>(A, a, b.cls, row, s, active && gl == 0, lds);
 }
 
-// Sliced rows: the row sum is a fixed tree over the 8 slice partials.
+// The row launch (PageRank.java:139-145 reduceByKey(Sum) + mapValues, and the inputs of
+// :113 and :125-134 for the next round).
 template <int MODE>
-__device__ __forceinline__ void combine_tile(const StepArgs& A, double a, const Bin& b,
-                                             uint32_t blk, uint64_t (*lds)[REC_WORDS]) {
-  const uint32_t i = blk * BLOCK + threadIdx.x;
-  const uint32_t row = b.row_begin + i;
-  const bool active = row < b.row_end;
-  double c = 0.0;
-  if (active) {
-    const uint32_t sr = b.srow_begin + i;
-    const double* p = A.part + sr;
-    const uint64_t S = A.nS;
-    c = ((p[0] + p[S]) + (p[2 * S] + p[3 * S])) + ((p[4 * S] + p[5 * S]) + (p[6 * S] + p[7 * S]));
-  }
-  row_epilogue<MODE>(A, a, b.cls, row, c, active, lds);
-}
-
-template <int MODE, int NT>
-__global__ __launch_bounds__(BLOCK) void spmv_round(StepArgs A) {
+__global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   __shared__ uint64_t lds[4][REC_WORDS];
   __shared__ double red[4];
-  const uint32_t b = blockIdx.x + A.block_base;
+  const uint32_t b = blockIdx.x;
   const Bin bin = A.bins[find_bin(A.bins, A.nbins, b)];
   const uint32_t blk = b - bin.block_begin;
   const double a = A.st->a;
   switch (bin.kind) {
-    case 0: group_tile<1, MODE, NT>(A, a, bin, blk, lds); break;
-    case 1: group_tile<2, MODE, NT>(A, a, bin, blk, lds); break;
-    case 2: group_tile<4, MODE, NT>(A, a, bin, blk, lds); break;
-    case 3: group_tile<8, MODE, NT>(A, a, bin, blk, lds); break;
-    case 4: group_tile<16, MODE, NT>(A, a, bin, blk, lds); break;
-    case 5: group_tile<32, MODE, NT>(A, a, bin, blk, lds); break;
-    case 6: group_tile<64, MODE, NT>(A, a, bin, blk, lds); break;
-    case KIND_COMBINE: combine_tile<MODE>(A, a, bin, blk, lds); break;
-    case KIND_BLOCK: {
+    case 0: group_tile<1, MODE>(A, a, bin, blk, lds); break;
+    case 1: group_tile<2, MODE>(A, a, bin, blk, lds); break;
+    case 2: group_tile<4, MODE>(A, a, bin, blk, lds); break;
+    case 3: group_tile<8, MODE>(A, a, bin, blk, lds); break;
+    case 4: group_tile<16, MODE>(A, a, bin, blk, lds); break;
+    case 5: group_tile<32, MODE>(A, a, bin, blk, lds); break;
+    case 6: group_tile<64, MODE>(A, a, bin, blk, lds); break;
+    default: {  // KIND_BLOCK: one workgroup per row
       const uint32_t row = bin.row_begin + blk;
-      double s = strided_sum<BLOCK, NT>(A.col, GatherX{A.x_in, A.colmask}, A.row_ptr[row],
-                                        A.row_ptr[row + 1], threadIdx.x);
+      double s = strided_sum<BLOCK, 1>(A.pidx, GatherX{A.partial}, A.row_pp[row],
+                                       A.row_pp[row + 1], threadIdx.x);
       s = block_sum(s, red);
       row_epilogue<MODE>(A, a, bin.cls, row, s, threadIdx.x == 0, lds);
       break;
     }
-    default: {  // KIND_HUB: one segment of an unsliced split row (combined in hub_round)
-      const HubSeg seg = A.segs[bin.seg_begin + blk];
-      double s = strided_sum<BLOCK, NT>(A.col, GatherX{A.x_in, A.colmask}, seg.e_begin,
-                                        seg.e_end, threadIdx.x);
-      s = block_sum(s, red);
-      if (threadIdx.x == 0) A.hub_part[seg.part] = s;
-      break;
-    }
   }
 }
 
-// ---- the slice launch: persistent, slice j = blockIdx % 8 (one XCD per slice) ----------
-// Every wave walks the wave-tiles of its slice with a static stride; a tile is 64/G rows of
-// a grouped bin, one (row, slice) sub-list of a long row, or one hub segment.  The first H
-// entries of the slice's x region (its hottest sources) are copied to LDS once per round.
-constexpr int SLICE_BLOCK = 1024;
-
-__device__ __forceinline__ double wave_sum(double s) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-  return s;
-}
-
-template <int G, int NT, class Gx>
-__device__ __forceinline__ void slice_group(const StepArgs& A, const Gx& gx, const Bin& b,
-                                            uint32_t tile, uint32_t j, int lane) {
-  constexpr uint32_t RPW = 64 / G;
-  const uint32_t i = tile * RPW + lane / G;
-  const uint32_t row = b.row_begin + i;
-  const int gl = lane % G;
-  const bool active = row < b.row_end;
-  double s = 0.0;
-  const uint32_t sr = b.srow_begin + i;
-  if (active) {
-    const uint64_t base = ld_stream<NT>(A.row_ptr + row);
-    const uint64_t beg = base + ld_stream<NT>(A.sb + static_cast<uint64_t>(j) * A.nS + sr);
-    const uint64_t end = base + ld_stream<NT>(A.sb + static_cast<uint64_t>(j + 1) * A.nS + sr);
-    s = strided_sum<G, NT>(A.col, gx, beg, end, gl);
-  }
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-  if (active && gl == 0) A.part[static_cast<uint64_t>(j) * A.nS + sr] = s;
-}
-
-template <int NT, class Gx>
-__device__ __forceinline__ void slice_tile(const StepArgs& A, const Gx& gx, uint32_t t,
-                                           uint32_t j, int lane) {
-  const Bin bin = A.bins[find_bin(A.bins, A.nbins, t)];
-  const uint32_t tt = t - bin.block_begin;
-  switch (bin.kind) {
-    case 0: slice_group<1, NT>(A, gx, bin, tt, j, lane); break;
-    case 1: slice_group<2, NT>(A, gx, bin, tt, j, lane); break;
-    case 2: slice_group<4, NT>(A, gx, bin, tt, j, lane); break;
-    case 3: slice_group<8, NT>(A, gx, bin, tt, j, lane); break;
-    case 4: slice_group<16, NT>(A, gx, bin, tt, j, lane); break;
-    case 5: slice_group<32, NT>(A, gx, bin, tt, j, lane); break;
-    case 6: slice_group<64, NT>(A, gx, bin, tt, j, lane); break;
-    case KIND_BLOCK: {  // one long (row, slice) sub-list per wave
-      const uint32_t row = bin.row_begin + tt;
-      const uint32_t sr = bin.srow_begin + tt;
-      const uint64_t base = A.row_ptr[row];
-      const uint64_t beg = base + A.sb[static_cast<uint64_t>(j) * A.nS + sr];
-      const uint64_t end = base + A.sb[static_cast<uint64_t>(j + 1) * A.nS + sr];
-      const double s = wave_sum(strided_sum<64, NT>(A.col, gx, beg, end, lane));
-      if (lane == 0) A.part[static_cast<uint64_t>(j) * A.nS + sr] = s;
-      break;
-    }
-    default: {  // KIND_HUB: slice j's segment list (padded with empty segments)
-      const HubSeg seg = A.segs[static_cast<uint64_t>(j) * A.hub_tiles + bin.seg_begin + tt];
-      const double s = wave_sum(strided_sum<64, NT>(A.col, gx, seg.e_begin, seg.e_end, lane));
-      if (lane == 0 && seg.part != 0xFFFFFFFFu) A.hub_part[seg.part] = s;
-      break;
-    }
-  }
-}
+// ---- the stream launch: persistent, slice j = blockIdx % 8 (one XCD per slice) ----------
+// Slice j's stream is cut into tasks of TASK = 1024 edges; wave w of the XCD takes tasks
+// w, w + W, w + 2W, ... (W = waves per XCD), so the XCD sweeps the stream front to back and
+// its L2 holds the segment being swept.  Lane i of a task owns edges [16i, 16i+16): four
+// 16-byte column loads, a 16-bit pair-start mask, sixteen independent gathers (the first H
+// entries of the slice's region from an LDS copy).  Pieces are summed in edge order inside
+// a lane; pieces that cross lanes are joined by a segmented scan over the wave.  Every
+// summation order is fixed by the stream layout (deterministic).
+struct StreamArgs {
+  const uint32_t* col;
+  const uint16_t* bits;
+  const uint32_t* task_piece;
+  const double* x_in;
+  double* partial;
+  uint64_t sbase[NSLICE];    // first stream edge of slice j (multiple of TASK)
+  uint64_t slen[NSLICE];     // edges of slice j
+  uint32_t tbase[NSLICE];    // first global task of slice j
+  uint32_t hot_base[NSLICE]; // x position of each slice region's start
+  uint32_t hot_n;            // x entries per slice served from LDS
+  uint32_t colmask;          // PR_COLMASK (timing experiments only)
+  uint32_t dbg;              // PR_DBG timing experiments: 1 no stores, 2 no gathers, 4 no starts
+};
+constexpr int STREAM_BLOCK = 1024;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <int NT, bool HOT>
-__global__ __launch_bounds__(SLICE_BLOCK) void spmv_slices(StepArgs A) {
+__global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
-  const uint32_t j = blockIdx.x % NSLICE, bi = blockIdx.x / NSLICE;
-  const uint32_t nb = gridDim.x / NSLICE, nw = blockDim.x / 64;
+  const uint32_t j = blockIdx.x % NSLICE;
+  const uint32_t wpb = blockDim.x >> 6;
   const int lane = threadIdx.x & 63;
-  const uint32_t w0 = bi * nw + threadIdx.x / 64, stride = nb * nw;
+  const uint32_t w = (blockIdx.x / NSLICE) * wpb + (threadIdx.x >> 6);
+  const uint32_t nw = (gridDim.x / NSLICE) * wpb;
+  const uint32_t base = A.hot_base[j];
+  const uint32_t H = HOT ? A.hot_n : 0u;
+  const double* __restrict__ x = A.x_in;
   if constexpr (HOT) {
-    const uint32_t base = A.hot_base[j], H = A.hot_n;
-    for (uint32_t i = threadIdx.x; i < H; i += blockDim.x) hot[i] = A.x_in[base + i];
+    for (uint32_t i = threadIdx.x; i < H; i += blockDim.x) hot[i] = x[base + i];
     __syncthreads();
-    const GatherLds gx{A.x_in, hot, base, H, A.colmask};
-    for (uint32_t t = A.block_base + w0; t < A.tile_end; t += stride) slice_tile<NT>(A, gx, t, j, lane);
-  } else {
-    const GatherX gx{A.x_in, A.colmask};
-    for (uint32_t t = A.block_base + w0; t < A.tile_end; t += stride) slice_tile<NT>(A, gx, t, j, lane);
   }
-}
-
-// Split rows: sum the segment partials in segment order, then the same epilogue.
-template <int MODE>
-__global__ __launch_bounds__(BLOCK) void hub_round(StepArgs A) {
-  __shared__ uint64_t lds[4][REC_WORDS];
-  __shared__ double red[4];
-  const HubRow h = A.hubs[blockIdx.x];
-  double s = 0.0;
-  for (uint32_t i = h.part_begin + threadIdx.x; i < h.part_end; i += BLOCK) s += A.hub_part[i];
-  s = block_sum(s, red);
-  row_epilogue<MODE>(A, A.st->a, h.cls, h.row, s, threadIdx.x == 0, lds);
+  const uint64_t len = A.slen[j];
+  const uint32_t ntask = static_cast<uint32_t>((len + TASK - 1) / TASK);
+  const uint32_t* __restrict__ colj = A.col + A.sbase[j];
+  const uint16_t* __restrict__ bitsj = A.bits + A.sbase[j] / EPL;
+  const uint32_t* __restrict__ tpj = A.task_piece + A.tbase[j];
+  double* __restrict__ part = A.partial;
+  const uint32_t cm = A.colmask;
+  // software pipeline: the next task's stream words are in flight while this task gathers
+  u32x4 cn[4];
+  uint32_t bnx = 0, tpn = 0;
+  auto fetch = [&](uint32_t tt) {
+    const uint64_t o = static_cast<uint64_t>(tt) * TASK + lane * EPL;
+    // the stream buffer is padded to whole tasks: these loads never leave it
+    const u32x4* cp = reinterpret_cast<const u32x4*>(colj + o);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cn[q] = ld_stream<NT>(cp + q);
+    bnx = ld_stream<NT>(bitsj + o / EPL);
+    tpn = tpj[tt];
+  };
+  if (w < ntask) fetch(w);
+  for (uint32_t t = w; t < ntask; t += nw) {
+    const uint64_t off = static_cast<uint64_t>(t) * TASK;
+    const uint64_t rem = len - off;
+    const int nval = rem >= static_cast<uint64_t>(TASK) ? TASK : static_cast<int>(rem);
+    const int lo = lane * EPL;
+    const int nv = min(max(nval - lo, 0), EPL);
+    u32x4 cv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cv[q] = cn[q];
+    uint32_t b = bnx;
+    const uint32_t tp0 = tpn;
+    if (A.dbg & 4u) b = 0;
+    if (lane == 0) b |= 1u;                       // a task always starts a piece
+    b &= nv >= EPL ? 0xFFFFu : ((1u << nv) - 1u);  // no starts past the stream end
+    // Sixteen gathers issued back to back, no branches: a hot source reads its LDS copy and
+    // points its (then redundant) global load at the slice's first entry, which every hot
+    // lane of the instruction shares (one request); padding edges read x[0] and are masked.
+    double v[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const uint32_t q = cv[k >> 2][k & 3] & cm;
+      if (A.dbg & 2u) {
+        v[k] = static_cast<double>(q);
+      } else if constexpr (HOT) {
+        const uint32_t o = q - base;
+        const bool h = o < H;
+        const double lv = hot[h ? o : 0u];
+        const double gv = x[h ? base : q];
+        v[k] = h ? lv : gv;
+      } else {
+        v[k] = x[q];
+      }
+    }
+    // next task's stream words, issued after the gathers so that waiting for the gathers
+    // (vmcnt counts in issue order) leaves them in flight
+    fetch(min(t + nw, ntask - 1));
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) v[k] = k < nv ? v[k] : 0.0;
+    // exclusive prefix (over lanes) of the piece starts -> first piece index of this lane
+    const int cnt = __popc(b);
+    int C = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(C, d);
+      if (lane >= d) C += y;
+    }
+    uint32_t pc = tp0 + static_cast<uint32_t>(C - cnt) - 1u;  // piece open before edge 0
+    // pass over the lane's edges: pieces complete inside the lane are written here
+    double run = 0.0, head = 0.0;
+    bool in_head = (b & 1u) == 0u;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      if ((b >> k) & 1u) {
+        if (k > 0) {
+          if (in_head) head = run;
+          else if (!(A.dbg & 1u)) part[pc] = run;
+          in_head = false;
+        }
+        ++pc;
+        run = 0.0;
+      }
+      run += v[k];
+    }
+    // segmented inclusive scan of the open piece over lanes (flag: lane holds a start)
+    double S = run;
+    bool F = b != 0u || nv == 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double Su = __shfl_up(S, d);
+      const int Fu = __shfl_up(static_cast<int>(F), d);
+      if (lane >= d) {
+        if (!F) S = Su + S;
+        F = F || Fu != 0;
+      }
+    }
+    const double carry = __shfl_up(S, 1);
+    const uint32_t bn = __shfl_down(b, 1);
+    const int nvn = __shfl_down(nv, 1);
+    const bool closes = lane == 63 || nvn == 0 || (bn & 1u) != 0u;  // next edge starts a piece
+    if (nv > 0 && !(A.dbg & 1u)) {
+      if (b == 0u) {
+        if (closes) part[pc] = S;                     // lane inside a longer piece
+      } else {
+        if (!(b & 1u)) part[tp0 + static_cast<uint32_t>(C - cnt) - 1u] = carry + head;
+        if (closes) part[pc] = run;                   // the lane's last piece
+      }
+    }
+  }
 }
 
 // Sum the NSHARD shards into one record and clear them for the next round.
@@ -688,28 +695,70 @@ __global__ void k_x_init(const uint32_t* perm, const uint32_t* outdeg, uint32_t 
   if (col) x_init[xpos(L, k)] = 1.0 / static_cast<double>(outdeg[perm[k]]);
 }
 
-// relabel unique edges to (local row, slice, internal source) and keep this rank's rows;
-// rows with in-degree >= ks get their edges grouped by the slice of the source's x line
-__global__ void k_relabel(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv,
-                          const uint32_t* indeg, uint32_t ks, Layout L,
-                          unsigned long long* counter, uint64_t* out) {
+// ---- slice streams -----------------------------------------------------------------------
+// q-space of a slice: class-A columns [0, SLq) in hotness order, then class-C columns.
+struct StreamGeo {
+  uint32_t SLq;       // q-space length of the class-A part of one slice
+  uint32_t QH, S;     // hot segment length, cold segment length (x entries)
+  int qb, rb, sgb;    // key fields: q within segment | local row | segment | slice
+};
+__device__ __forceinline__ void col_slice_q(const Layout& L, const StreamGeo& G, uint32_t k,
+                                            uint32_t& sl, uint32_t& q) {
+  if (k < L.nA) {
+    const uint32_t c = k / CHUNK;
+    sl = c % NSLICE;
+    q = (c / NSLICE) * CHUNK + k % CHUNK;
+  } else {
+    const uint32_t kc = k - L.R, c = kc / CHUNK;
+    sl = c % NSLICE;
+    q = G.SLq + (c / NSLICE) * CHUNK + kc % CHUNK;
+  }
+}
+__device__ __forceinline__ uint32_t col_of_slice_q(const Layout& L, const StreamGeo& G,
+                                                   uint32_t sl, uint32_t q) {
+  if (q < G.SLq) return ((q / CHUNK) * NSLICE + sl) * CHUNK + q % CHUNK;
+  const uint32_t qc = q - G.SLq;
+  return L.R + ((qc / CHUNK) * NSLICE + sl) * CHUNK + qc % CHUNK;
+}
+// internal column id of an x position (inverse of xpos)
+__device__ __forceinline__ uint32_t col_of_xpos(const Layout& L, uint32_t x) {
+  const uint32_t PA = L.p * L.maxA;
+  if (x < PA) {
+    const uint32_t r = x / L.maxA, y = x % L.maxA;
+    if (!L.sm) return ((y / CHUNK) * L.p + r) * CHUNK + y % CHUNK;
+    const uint32_t sl = (y / L.SL) * L.p + r, rem = y % L.SL;
+    return ((rem / CHUNK) * NSLICE + sl) * CHUNK + rem % CHUNK;
+  }
+  const uint32_t qc = x - PA;
+  if (!L.sm) return L.R + qc;
+  const uint32_t sl = qc / L.SLC, rem = qc % L.SLC;
+  return L.R + ((rem / CHUNK) * NSLICE + sl) * CHUNK + rem % CHUNK;
+}
+
+// relabel unique edges to stream keys (slice, segment, local row, q within segment) and keep
+// this rank's rows (wave-aggregated append when p > 1)
+__global__ void k_stream_keys(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv,
+                              Layout L, StreamGeo G, unsigned long long* counter, uint64_t* out) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   bool keep = false;
   uint64_t key = 0;
   if (e < nnz) {
     const uint64_t k = uk[e];
-    const uint32_t d = static_cast<uint32_t>(k >> nb);
-    const uint32_t kd = inv[d];
-    const uint32_t ksrc = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
+    const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
+    const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
     keep = owner_of(L, kd) == L.rank;
-    const uint64_t sl = indeg[d] >= ks ? slice_of(L, ksrc) : 0u;
-    key = (static_cast<uint64_t>(local_of(L, kd)) << (nb + 3)) | (sl << nb) | ksrc;
+    uint32_t sl, q;
+    col_slice_q(L, G, ks, sl, q);
+    const uint32_t seg = q < G.QH ? 0u : 1u + (q - G.QH) / G.S;
+    const uint32_t qin = seg ? (q - G.QH) % G.S : q;
+    key = (static_cast<uint64_t>(sl) << (G.sgb + G.rb + G.qb)) |
+          (static_cast<uint64_t>(seg) << (G.rb + G.qb)) |
+          (static_cast<uint64_t>(local_of(L, kd)) << G.qb) | qin;
   }
   if (L.p == 1) {
     if (e < nnz) out[e] = key;
     return;
   }
-  // wave-aggregated append
   const uint64_t mask = __ballot(keep);
   if (!mask) return;
   const int lane = threadIdx.x & 63;
@@ -720,55 +769,145 @@ __global__ void k_relabel(const uint64_t* uk, uint64_t nnz, int nb, const uint32
   if (keep) out[base + __popcll(mask & ((1ull << lane) - 1))] = key;
 }
 
-struct SliceRows {
-  uint32_t lA, sA, sB, nS;
-};
-__device__ __forceinline__ int srow_of(const SliceRows& S, uint32_t l) {
-  if (l < S.sA) return static_cast<int>(l);
-  if (l >= S.lA && l - S.lA < S.sB) return static_cast<int>(S.sA + (l - S.lA));
-  return -1;
-}
-
-// col = x position of the source; per (sliced row, slice) edge counts
-__global__ void k_col(const uint64_t* lk, uint64_t lnnz, int nb, Layout L, SliceRows S,
-                      uint32_t* col, uint32_t* cnt) {
+// first sorted edge of each slice (atomicMin; slices without edges keep the sentinel)
+__global__ void k_slice_starts(const uint64_t* key, uint64_t n, int shift,
+                               unsigned long long* starts) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (e >= lnnz) return;
-  const uint64_t key = lk[e];
-  col[e] = xpos(L, static_cast<uint32_t>(key & ((1ull << nb) - 1)));
-  const int sr = srow_of(S, static_cast<uint32_t>(key >> (nb + 3)));
-  if (sr >= 0) {
-    const uint32_t sl = static_cast<uint32_t>((key >> nb) & 7);
-    atomicAdd(&cnt[static_cast<uint64_t>(sl) * S.nS + sr], 1u);
-  }
+  if (e >= n) return;
+  const uint32_t sl = static_cast<uint32_t>(key[e] >> shift);
+  if (e == 0 || static_cast<uint32_t>(key[e - 1] >> shift) != sl)
+    atomicMin(&starts[sl], static_cast<unsigned long long>(e));
 }
 
-// sb[j][srow] = edges of the row in slices < j (relative to the row start)
-__global__ void k_slice_prefix(const uint32_t* cnt, uint32_t nS, uint32_t* sb) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nS) return;
-  uint32_t acc = 0;
-  for (int j = 0; j < NSLICE; ++j) {
-    sb[static_cast<uint64_t>(j) * nS + r] = acc;
-    acc += cnt[static_cast<uint64_t>(j) * nS + r];
-  }
-  sb[static_cast<uint64_t>(NSLICE) * nS + r] = acc;
+struct StreamPos {
+  uint64_t start[NSLICE + 1];  // first sorted edge of slice j
+  uint64_t sbase[NSLICE];      // first stream position of slice j
+  uint32_t tbase[NSLICE + 1];  // first global task of slice j
+};
+__device__ __forceinline__ uint32_t slice_of_edge(const StreamPos& P, uint64_t e) {
+  uint32_t j = 0;
+#pragma unroll
+  for (int i = 1; i < NSLICE; ++i) j += e >= P.start[i] ? 1u : 0u;
+  return j;
 }
 
-__global__ void k_local_rows(const uint32_t* perm, const uint32_t* indeg, const uint32_t* outdeg,
-                             const uint32_t* dang_w, uint32_t lrows, uint32_t lA, Layout L,
-                             uint64_t* deg64, uint32_t* ldeg, uint32_t* meta) {
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l > lrows) return;
-  if (l == lrows) {
-    deg64[l] = 0;
+// col (x position) of every stream edge + the pair-start flags
+__global__ void k_stream_fill(const uint64_t* key, uint64_t n, Layout L, StreamGeo G,
+                              StreamPos P, uint32_t* col, uint32_t* bits32,
+                              unsigned long long* n_pairs) {
+  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  bool start = false;
+  if (e < n) {
+    const uint64_t k = key[e];
+    const uint32_t sl = slice_of_edge(P, e);
+    const uint64_t pos = P.sbase[sl] + (e - P.start[sl]);
+    const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
+    const uint32_t qin = static_cast<uint32_t>(k & ((1ull << G.qb) - 1));
+    const uint32_t q = seg ? G.QH + (seg - 1) * G.S + qin : qin;
+    col[pos] = xpos(L, col_of_slice_q(L, G, sl, q));
+    start = e == P.start[sl] || (key[e - 1] >> G.qb) != (k >> G.qb);
+    if (start) atomicOr(&bits32[pos / 32], 1u << (pos % 32));
+  }
+  const uint64_t s = wave_sum_u64(start ? 1u : 0u);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(n_pairs, static_cast<unsigned long long>(s));
+}
+
+// pieces of each task (piece starts: the task's first edge and every pair start)
+__global__ void k_task_count(const uint32_t* bits32, StreamPos P, uint32_t ntask, uint32_t* cnt) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntask) return;
+  if (t == ntask) {
+    cnt[t] = 0;
     return;
   }
+  uint32_t j = 0;
+  for (int i = 1; i < NSLICE; ++i) j += t >= P.tbase[i] ? 1u : 0u;
+  const uint64_t w0 = (P.sbase[j] + static_cast<uint64_t>(t - P.tbase[j]) * TASK) / 32;
+  uint32_t c = 0;
+  for (int i = 0; i < TASK / 32; ++i) c += __popc(bits32[w0 + i] | (i == 0 ? 1u : 0u));
+  cnt[t] = c;
+}
+
+// piece index of stream position pos (slice j); also whether pos starts a piece
+__device__ __forceinline__ uint32_t piece_of(const uint32_t* bits32, const uint32_t* task_piece,
+                                             const StreamPos& P, uint32_t j, uint64_t pos,
+                                             bool* starts) {
+  const uint64_t rel = pos - P.sbase[j];
+  const uint64_t tl = rel / TASK;
+  const uint64_t w0 = (P.sbase[j] + tl * TASK) / 32, wp = pos / 32;
+  const uint32_t bit = static_cast<uint32_t>(pos % 32);
+  uint32_t c = 0;
+  for (uint64_t w = w0; w < wp; ++w) c += __popc(bits32[w] & (w == w0 ? ~1u : ~0u));
+  const uint32_t last = bits32[wp] & (wp == w0 ? ~1u : ~0u);
+  c += __popc(last & (bit == 31 ? ~0u : ((2u << bit) - 1u)));
+  if (starts) *starts = (rel % TASK) == 0 || ((bits32[wp] >> bit) & 1u);
+  return task_piece[P.tbase[j] + tl] + c;
+}
+
+// row of every piece (from the stream keys)
+__global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, StreamPos P,
+                             const uint32_t* bits32, const uint32_t* task_piece,
+                             uint32_t* piece_row) {
+  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t sl = slice_of_edge(P, e);
+  const uint64_t pos = P.sbase[sl] + (e - P.start[sl]);
+  bool st = false;
+  const uint32_t pc = piece_of(bits32, task_piece, P, sl, pos, &st);
+  if (st) piece_row[pc] = static_cast<uint32_t>(key[e] >> G.qb) & ((1u << G.rb) - 1u);
+}
+
+__global__ void k_fill_f64(double* a, uint64_t n, double v) {
+  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (i < n) a[i] = v;
+}
+
+__global__ void k_iota(uint32_t* a, uint64_t n) {
+  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (i < n) a[i] = static_cast<uint32_t>(i);
+}
+
+// row_pp[r] = first position of row r in the row-sorted piece list (every row has one)
+__global__ void k_row_starts(const uint32_t* rows_sorted, uint64_t n, uint32_t* row_pp) {
+  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (i >= n) return;
+  if (i == 0 || rows_sorted[i - 1] != rows_sorted[i]) row_pp[rows_sorted[i]] = static_cast<uint32_t>(i);
+}
+
+__global__ void k_local_meta(const uint32_t* perm, const uint32_t* outdeg, const uint32_t* dang_w,
+                             uint32_t lrows, uint32_t lA, Layout L, uint32_t* meta) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= lrows) return;
   const uint32_t v = perm[row_of(L, l)];
-  const uint32_t d = indeg[v];
-  deg64[l] = d;
-  ldeg[l] = d;
   meta[l] = l < lA ? outdeg[v] : dang_w[v];
+}
+
+// export: (internal row << 32 | internal source) of every stream edge
+__global__ void k_piece_row_of(const uint32_t* row_pp, const uint32_t* pidx, uint32_t lrows,
+                               uint32_t* piece_row) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= lrows) return;
+  for (uint32_t k = row_pp[l]; k < row_pp[l + 1]; ++k) piece_row[pidx[k]] = l;
+}
+__global__ void k_export_keys(const uint32_t* col, const uint32_t* bits32,
+                              const uint32_t* task_piece, const uint32_t* piece_row, Layout L,
+                              StreamPos P, uint64_t stream_len, uint64_t* out) {
+  const uint64_t pos = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (pos >= stream_len) return;
+  uint32_t j = 0;
+  for (int i = 1; i < NSLICE; ++i) j += pos >= P.sbase[i] ? 1u : 0u;
+  const uint64_t rel = pos - P.sbase[j];
+  if (rel >= P.start[j + 1] - P.start[j]) return;  // padding
+  const uint32_t pc = piece_of(bits32, task_piece, P, j, pos, nullptr);
+  const uint32_t row = row_of(L, piece_row[pc]);
+  out[P.start[j] + rel] = (static_cast<uint64_t>(row) << 32) | col_of_xpos(L, col[pos]);
+}
+__global__ void k_export_split(const uint64_t* key, uint64_t n, uint32_t* col, uint64_t* row_ptr) {
+  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = key[i];
+  col[i] = static_cast<uint32_t>(k);
+  if (i == 0 || (key[i - 1] >> 32) != (k >> 32)) row_ptr[k >> 32] = i;
 }
 
 __global__ void k_scatter_ranks(const uint32_t* perm, const double* r_loc, uint32_t lrows,
@@ -832,12 +971,10 @@ int env_int(const char* name, int def) {
 
 void dev_free(DevGraph* g) {
   auto F = [](void* p) { if (p) (void)hipFree(p); };
-  F(g->row_ptr); F(g->col); F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
-  F(g->sb); F(g->part);
+  F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->row_pp); F(g->pidx);
+  F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
-  F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->d_bins); F(g->d_sbins);
-  F(g->d_hubs); F(g->d_segs); F(g->d_ssegs); F(g->hub_part);
-  for (auto e : g->split_ev) (void)hipEventDestroy(e);
+  F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->d_bins);
   const int p = g->p, rank = g->rank;
   *g = DevGraph();
   g->p = p;
@@ -876,12 +1013,12 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   Tuning& T = g->tune;
   T.epl = std::max(1, env_int("PR_EPL", T.epl));
   T.kb = static_cast<uint32_t>(std::max(64, env_int("PR_KB", static_cast<int>(T.kb))));
-  T.kh = static_cast<uint32_t>(std::max(static_cast<int>(T.kb), env_int("PR_KH", static_cast<int>(T.kh))));
-  T.seg = static_cast<uint32_t>(std::max(256, env_int("PR_SEG", static_cast<int>(T.seg))));
-  T.ks = static_cast<uint32_t>(std::max(1, env_int("PR_KS", static_cast<int>(T.ks))));
+  T.qh = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_QH", static_cast<int>(T.qh))));
+  T.seg = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_SEG", static_cast<int>(T.seg))));
   T.nt = env_int("PR_NT", T.nt);
   T.hot_lds = static_cast<uint32_t>(std::max(0, std::min(20480, env_int("PR_HOTLDS", static_cast<int>(T.hot_lds)))));
-  T.split = env_int("PR_SPLIT", 0);
+  T.dbg = env_int("PR_DBG", 0);
+  T.stream_wg = std::max(1, std::min(2, env_int("PR_STREAM_WG", T.stream_wg)));
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   const uint32_t n = in.n;
   const uint64_t m = in.m;
@@ -889,13 +1026,11 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   g->m_raw = m;
   g->n_tot = in.n_tot;
   const int nb = in.rmat ? std::max(1, in.scale) : bits_for(n);
-  // edge keys (local row, slice, source) take 2*nb + 3 bits
-  if (2 * nb + 3 > 64) {
-    if (err) *err = "more than 2^30 vertices is not supported (64-bit edge keys)";
+  // raw edge keys (dst, src) take 2*nb bits
+  if (2 * nb > 64) {
+    if (err) *err = "more than 2^32 vertices is not supported (64-bit edge keys)";
     return PR_E_ARG;
   }
-  const uint32_t ks = T.ks;
-  const int key_bits = 2 * nb + 3;
   Temp tmp;
 
   // ---- raw keys (dst << nb | src) ------------------------------------------------------
@@ -1038,225 +1173,175 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   uint32_t* inv = vid;  // reuse: n entries
   if (n) hipLaunchKernelGGL(k_inverse, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->perm, n, inv);
 
-  // ---- per-row data: in-degrees (host copy for the schedule), meta, row pointers --------
+  // ---- per-row data ------------------------------------------------------------------------
   const uint32_t lrows = g->lrows;
-  uint64_t* deg64 = nullptr;
-  uint32_t* ldeg = nullptr;
-  TRY(dmalloc(&deg64, lrows + 1ull, err));
-  TRY(dmalloc(&ldeg, lrows, err));
   TRY(dmalloc(&g->meta, lrows, err));
-  TRY(dmalloc(&g->row_ptr, lrows + 1ull, err));
-  hipLaunchKernelGGL(k_local_rows, dim3(grid_for(lrows + 1ull)), dim3(BLOCK), 0, s, g->perm, g->indeg, g->outdeg, g->dang_w, lrows, g->lA, L, deg64, ldeg, g->meta);
-  {
-    size_t tb = 0;
-    HIPTRY(rocprim::exclusive_scan(nullptr, tb, deg64, g->row_ptr, uint64_t(0), lrows + 1ull, rocprim::plus<uint64_t>(), s));
-    TRY(tmp.ensure(tb, err));
-    HIPTRY(rocprim::exclusive_scan(tmp.p, tb, deg64, g->row_ptr, uint64_t(0), lrows + 1ull, rocprim::plus<uint64_t>(), s));
-  }
-  std::vector<uint32_t> hdeg(lrows);
-  if (lrows) HIPTRY(hipMemcpyAsync(hdeg.data(), ldeg, 4ull * lrows, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipStreamSynchronize(s));
-  (void)hipFree(deg64);
-  (void)hipFree(ldeg);
-  std::vector<uint64_t> hrow(lrows + 1ull, 0);
-  for (uint32_t l = 0; l < lrows; ++l) hrow[l + 1] = hrow[l] + hdeg[l];
-  // rows are sorted by in-degree (descending) inside each class: sliced rows and hubs lead
-  auto lead = [&](uint32_t b, uint32_t e, uint64_t thr) {
-    uint32_t i = b;
-    while (i < e && hdeg[i] >= thr) ++i;
-    return i - b;
-  };
-  g->sA = lead(0, g->lA, ks);
-  g->sB = lead(g->lA, lrows, ks);
-  g->hA = std::min(g->sA, lead(0, g->lA, T.kh + 1ull));
-  g->hB = std::min(g->sB, lead(g->lA, lrows, T.kh + 1ull));
-  g->nS = g->sA + g->sB;
-  const SliceRows SR{g->lA, g->sA, g->sB, g->nS};
+  if (lrows) hipLaunchKernelGGL(k_local_meta, dim3(grid_for(lrows)), dim3(BLOCK), 0, s, g->perm, g->outdeg, g->dang_w, lrows, g->lA, L, g->meta);
 
-  // ---- local edges: relabel, keep own rows, sort by (local row, slice, source) ----------
+  // ---- stream geometry -----------------------------------------------------------------------
+  StreamGeo G{};
+  {
+    const uint32_t chA = (g->nA + CHUNK - 1) / CHUNK, chC = (g->nC + CHUNK - 1) / CHUNK;
+    G.SLq = CHUNK * ((chA + NSLICE - 1) / NSLICE);
+    const uint64_t qtot = static_cast<uint64_t>(G.SLq) + CHUNK * ((chC + NSLICE - 1) / NSLICE);
+    G.S = T.seg;
+    G.QH = static_cast<uint32_t>(std::min<uint64_t>(T.qh, std::max<uint64_t>(qtot, 1)));
+    g->nseg = 1u + (qtot > G.QH ? static_cast<uint32_t>((qtot - G.QH + G.S - 1) / G.S) : 0u);
+    G.qb = bits_for(std::max(G.QH, G.S));
+    G.rb = bits_for(std::max<uint64_t>(lrows, 2));
+    G.sgb = bits_for(std::max<uint64_t>(g->nseg, 2));
+  }
+  const int key_bits = 3 + G.sgb + G.rb + G.qb;
+  if (key_bits > 64) {
+    if (err) *err = "stream keys need more than 64 bits (raise PR_SEG)";
+    return PR_E_ARG;
+  }
+
+  // ---- local edges: stream keys, stable radix sort -------------------------------------------
   uint64_t* lk_in = uniq == kA ? kB : kA;  // free buffer
-  unsigned long long* d_lc = nullptr;
-  TRY(dmalloc(&d_lc, 1, err));
-  HIPTRY(hipMemsetAsync(d_lc, 0, 8, s));
-  if (nnz) hipLaunchKernelGGL(k_relabel, dim3(grid_for(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, g->indeg, ks, L, d_lc, lk_in);
+  unsigned long long* d_cnt = nullptr;     // [0] local edges [1] pairs [2..10] slice starts
+  TRY(dmalloc(&d_cnt, 2 + NSLICE, err));
+  HIPTRY(hipMemsetAsync(d_cnt, 0, 16, s));
+  HIPTRY(hipMemsetAsync(d_cnt + 2, 0xFF, 8 * NSLICE, s));
+  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_for(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, d_cnt, lk_in);
   uint64_t lnnz = nnz;
   if (p > 1) {
-    HIPTRY(hipMemcpyAsync(&lnnz, d_lc, 8, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(&lnnz, d_cnt, 8, hipMemcpyDeviceToHost, s));
     HIPTRY(hipStreamSynchronize(s));
   }
-  (void)hipFree(d_lc);
   g->lnnz = lnnz;
-  uint64_t* lk_sorted = nullptr;
+  uint64_t* lk = nullptr;
   {
     rocprim::double_buffer<uint64_t> db(lk_in, uniq);
     size_t tb = 0;
     HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, lnnz, 0, key_bits, s));
     TRY(tmp.ensure(tb, err));
     if (lnnz) HIPTRY(rocprim::radix_sort_keys(tmp.p, tb, db, lnnz, 0, key_bits, s));
-    lk_sorted = db.current();
+    lk = db.current();
   }
-  TRY(dmalloc(&g->col, lnnz, err));
-  uint32_t* cnt = nullptr;
-  TRY(dmalloc(&cnt, static_cast<size_t>(NSLICE) * g->nS, err));
-  if (g->nS) HIPTRY(hipMemsetAsync(cnt, 0, 4ull * NSLICE * g->nS, s));
-  if (lnnz) hipLaunchKernelGGL(k_col, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk_sorted, lnnz, nb, L, SR, g->col, cnt);
-  TRY(dmalloc(&g->sb, (NSLICE + 1ull) * g->nS, err));
-  if (g->nS) hipLaunchKernelGGL(k_slice_prefix, dim3(grid_for(g->nS)), dim3(BLOCK), 0, s, cnt, g->nS, g->sb);
+  const int sl_shift = G.sgb + G.rb + G.qb;
+  if (lnnz) hipLaunchKernelGGL(k_slice_starts, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, sl_shift, d_cnt + 2);
+  unsigned long long hst[NSLICE];
+  HIPTRY(hipMemcpyAsync(hst, d_cnt + 2, 8 * NSLICE, hipMemcpyDeviceToHost, s));
   HIPTRY(hipStreamSynchronize(s));
+  StreamPos SP{};
+  SP.start[NSLICE] = lnnz;
+  for (int j = NSLICE - 1; j >= 0; --j) SP.start[j] = std::min<uint64_t>(hst[j], SP.start[j + 1]);
+  uint64_t pos = 0;
+  uint32_t tasks = 0;
+  for (int j = 0; j < NSLICE; ++j) {
+    g->slen[j] = SP.start[j + 1] - SP.start[j];
+    g->sbase[j] = SP.sbase[j] = pos;
+    g->tbase[j] = SP.tbase[j] = tasks;
+    const uint64_t nt = (g->slen[j] + TASK - 1) / TASK;
+    if (tasks + nt > 0xFFFFFFFFull) {
+      if (err) *err = "too many stream tasks";
+      return PR_E_ARG;
+    }
+    tasks += static_cast<uint32_t>(nt);
+    pos += nt * TASK;
+  }
+  g->tbase[NSLICE] = SP.tbase[NSLICE] = tasks;
+  g->stream_len = pos;
+
+  // ---- stream arrays: col, pair-start flags, pieces ------------------------------------------
+  TRY(dmalloc(&g->col, g->stream_len, err));
+  TRY(dmalloc(&g->bits, g->stream_len / EPL + 2, err));
+  HIPTRY(hipMemsetAsync(g->col, 0, 4 * std::max<uint64_t>(g->stream_len, 1), s));
+  HIPTRY(hipMemsetAsync(g->bits, 0, 2 * (g->stream_len / EPL + 2), s));
+  uint32_t* bits32 = reinterpret_cast<uint32_t*>(g->bits);
+  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, SP, g->col, bits32, d_cnt + 1);
+  TRY(dmalloc(&g->task_piece, tasks + 1ull, err));
+  {
+    uint32_t* tcnt = nullptr;
+    TRY(dmalloc(&tcnt, tasks + 1ull, err));
+    hipLaunchKernelGGL(k_task_count, dim3(grid_for(tasks + 1ull)), dim3(BLOCK), 0, s, bits32, SP, tasks, tcnt);
+    size_t tb = 0;
+    HIPTRY(rocprim::exclusive_scan(nullptr, tb, tcnt, g->task_piece, 0u, tasks + 1ull, rocprim::plus<uint32_t>(), s));
+    TRY(tmp.ensure(tb, err));
+    HIPTRY(rocprim::exclusive_scan(tmp.p, tb, tcnt, g->task_piece, 0u, tasks + 1ull, rocprim::plus<uint32_t>(), s));
+    uint32_t np = 0;
+    unsigned long long npairs = 0;
+    HIPTRY(hipMemcpyAsync(&np, g->task_piece + tasks, 4, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(&npairs, d_cnt + 1, 8, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(tcnt);
+    g->n_pieces = np;
+    g->n_pairs = npairs;
+  }
+  const uint64_t NP = g->n_pieces;
+  {
+    uint32_t *prow = nullptr, *prow2 = nullptr, *ids = nullptr;
+    TRY(dmalloc(&prow, NP, err));
+    TRY(dmalloc(&prow2, NP, err));
+    TRY(dmalloc(&ids, NP, err));
+    TRY(dmalloc(&g->pidx, NP, err));
+    TRY(dmalloc(&g->row_pp, lrows + 1ull, err));
+    if (lnnz) hipLaunchKernelGGL(k_piece_rows, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, SP, bits32, g->task_piece, prow);
+    if (NP) hipLaunchKernelGGL(k_iota, dim3(grid_for(NP)), dim3(BLOCK), 0, s, ids, NP);
+    size_t tb = 0;
+    HIPTRY(rocprim::radix_sort_pairs(nullptr, tb, prow, prow2, ids, g->pidx, NP, 0, G.rb, s));
+    TRY(tmp.ensure(tb, err));
+    if (NP) HIPTRY(rocprim::radix_sort_pairs(tmp.p, tb, prow, prow2, ids, g->pidx, NP, 0, G.rb, s));
+    HIPTRY(hipMemsetAsync(g->row_pp, 0xFF, 4ull * (lrows + 1), s));
+    if (NP) hipLaunchKernelGGL(k_row_starts, dim3(grid_for(NP)), dim3(BLOCK), 0, s, prow2, NP, g->row_pp);
+    const uint32_t np32 = static_cast<uint32_t>(NP);
+    HIPTRY(hipMemcpyAsync(g->row_pp + lrows, &np32, 4, hipMemcpyHostToDevice, s));
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(prow);
+    (void)hipFree(prow2);
+    (void)hipFree(ids);
+  }
   HIPTRY(hipGetLastError());
-  (void)hipFree(cnt);
+  (void)hipFree(d_cnt);
   (void)hipFree(kA);
   (void)hipFree(kB);
   kA = kB = nullptr;
   (void)hipFree(vid);
-  TRY(dmalloc(&g->part, static_cast<size_t>(NSLICE) * g->nS, err));
+  TRY(dmalloc(&g->partial, NP, err));
+  // PR_DBG experiments may skip the partial stores: keep every rank defined
+  if (T.dbg && NP) hipLaunchKernelGGL(k_fill_f64, dim3(grid_for(NP)), dim3(BLOCK), 0, s, g->partial, NP, 1.0);
 
-  // ---- schedule ---------------------------------------------------------------------------
-  // hub rows' slice offsets on the host (sliced hubs are split per slice into segments)
-  std::vector<uint32_t> hsb;  // [9][hA+hB]
-  const uint32_t nh_s = g->hA + g->hB;
-  if (nh_s) {
-    hsb.resize((NSLICE + 1ull) * nh_s);
-    for (int j = 0; j <= NSLICE; ++j) {
-      if (g->hA) HIPTRY(hipMemcpyAsync(&hsb[j * nh_s], g->sb + static_cast<uint64_t>(j) * g->nS, 4ull * g->hA, hipMemcpyDeviceToHost, s));
-      if (g->hB) HIPTRY(hipMemcpyAsync(&hsb[j * nh_s + g->hA], g->sb + static_cast<uint64_t>(j) * g->nS + g->sA, 4ull * g->hB, hipMemcpyDeviceToHost, s));
-    }
+  // ---- row launch schedule: bins of equal lanes-per-row over the row-sorted piece counts ----
+  {
+    std::vector<uint32_t> hpp(lrows + 1ull);
+    HIPTRY(hipMemcpyAsync(hpp.data(), g->row_pp, 4ull * (lrows + 1), hipMemcpyDeviceToHost, s));
     HIPTRY(hipStreamSynchronize(s));
-  }
-  uint32_t next_part = 0;
-  // (a) slice launch over sliced rows: kinds by the expected per-slice length k/8
-  {
-    std::vector<std::vector<HubSeg>> lists(NSLICE);
-    uint32_t tiles = 0, hub_tiles = 0;
-    for (int cls = 0; cls < 2; ++cls) {
-      const uint32_t r0 = cls ? g->lA : 0;
-      const uint32_t nsl = cls ? g->sB : g->sA, nhub = cls ? g->hB : g->hA;
-      const uint32_t srow0 = cls ? g->sA : 0, hub_i0 = cls ? g->hA : 0;
-      if (nhub) {  // hub rows: per-slice segment lists, padded to equal length
-        Bin b{};
-        b.block_begin = tiles;
-        b.row_begin = r0;
-        b.row_end = r0 + nhub;
-        b.kind = KIND_HUB;
-        b.cls = static_cast<uint16_t>(cls);
-        b.seg_begin = hub_tiles;
-        b.srow_begin = srow0;
-        size_t before[NSLICE];
-        for (int j = 0; j < NSLICE; ++j) before[j] = lists[j].size();
-        for (uint32_t i = 0; i < nhub; ++i) {
-          const uint32_t l = r0 + i;
-          HubRow h{l, next_part, 0, static_cast<uint32_t>(cls)};
-          for (int j = 0; j < NSLICE; ++j) {
-            const uint64_t e0 = hrow[l] + hsb[j * nh_s + hub_i0 + i];
-            const uint64_t e1 = hrow[l] + hsb[(j + 1) * nh_s + hub_i0 + i];
-            for (uint64_t e = e0; e < e1; e += T.seg)
-              lists[j].push_back({e, std::min<uint64_t>(e + T.seg, e1), next_part++, 0});
-          }
-          h.part_end = next_part;
-          g->hubs.push_back(h);
-        }
-        size_t T_ = 0;
-        for (int j = 0; j < NSLICE; ++j) T_ = std::max(T_, lists[j].size() - before[j]);
-        for (int j = 0; j < NSLICE; ++j)
-          while (lists[j].size() - before[j] < T_) lists[j].push_back({0, 0, 0xFFFFFFFFu, 0});
-        tiles += static_cast<uint32_t>(T_);
-        hub_tiles += static_cast<uint32_t>(T_);
-        g->sbins.push_back(b);
-        g->sbin_edges.push_back(hrow[r0 + nhub] - hrow[r0]);
+    for (uint32_t l = 0; l < lrows; ++l)
+      if (hpp[l] >= hpp[l + 1]) {
+        if (err) *err = "internal: a local row without pieces";
+        return PR_E_HIP;
       }
-      uint32_t i = nhub;
-      while (i < nsl) {  // non-hub sliced rows: runs of equal kind
-        const uint16_t kd = kind_for((hdeg[r0 + i] + NSLICE - 1) / NSLICE, T);
-        uint32_t e = i + 1;
-        while (e < nsl && kind_for((hdeg[r0 + e] + NSLICE - 1) / NSLICE, T) == kd) ++e;
-        Bin b{};
-        b.block_begin = tiles;
-        b.row_begin = r0 + i;
-        b.row_end = r0 + e;
-        b.kind = kd;
-        b.cls = static_cast<uint16_t>(cls);
-        b.srow_begin = srow0 + i;
-        const uint32_t rows = e - i;
-        tiles += kd == KIND_BLOCK ? rows : (rows + (64u >> kd) - 1) / (64u >> kd);
-        g->sbins.push_back(b);
-        g->sbin_edges.push_back(hrow[r0 + e] - hrow[r0 + i]);
-        i = e;
-      }
-    }
-    g->slice_tiles = tiles;
-    g->hub_tiles = hub_tiles;
-    std::vector<HubSeg> flat(static_cast<size_t>(NSLICE) * hub_tiles);
-    for (int j = 0; j < NSLICE; ++j)
-      for (uint32_t t = 0; t < hub_tiles; ++t) flat[static_cast<size_t>(j) * hub_tiles + t] = lists[j][t];
-    TRY(dmalloc(&g->d_ssegs, flat.size(), err));
-    if (!flat.empty()) HIPTRY(hipMemcpyAsync(g->d_ssegs, flat.data(), flat.size() * sizeof(HubSeg), hipMemcpyHostToDevice, s));
-    TRY(dmalloc(&g->d_sbins, g->sbins.size(), err));
-    if (!g->sbins.empty()) HIPTRY(hipMemcpyAsync(g->d_sbins, g->sbins.data(), g->sbins.size() * sizeof(Bin), hipMemcpyHostToDevice, s));
-  }
-  // (b) row launch: combine bins for sliced non-hub rows, then unsliced rows by kind
-  {
-    struct Run { uint16_t kind, cls; uint32_t b, e, srow; };
-    std::vector<Run> runs;
-    for (int cls = 0; cls < 2; ++cls) {
-      const uint32_t r0 = cls ? g->lA : 0;
-      const uint32_t nsl = cls ? g->sB : g->sA, nhub = cls ? g->hB : g->hA;
-      const uint32_t srow0 = cls ? g->sA : 0;
-      if (nsl > nhub) runs.push_back({KIND_COMBINE, static_cast<uint16_t>(cls), r0 + nhub, r0 + nsl, srow0 + nhub});
-      const uint32_t e0 = cls ? lrows : g->lA;
-      uint32_t i = r0 + nsl;
-      while (i < e0) {
-        const uint16_t kd = hdeg[i] > T.kh ? static_cast<uint16_t>(KIND_HUB) : kind_for(hdeg[i], T);
-        uint32_t e = i + 1;
-        while (e < e0 && (hdeg[e] > T.kh ? static_cast<uint16_t>(KIND_HUB) : kind_for(hdeg[e], T)) == kd) ++e;
-        runs.push_back({kd, static_cast<uint16_t>(cls), i, e, 0});
-        i = e;
-      }
-    }
-    std::stable_sort(runs.begin(), runs.end(), [](const Run& a, const Run& b) {
-      auto w = [](uint16_t k) { return k == KIND_COMBINE ? 100 : static_cast<int>(k); };
-      return w(a.kind) > w(b.kind);
-    });
-    std::vector<HubSeg> segs;
     uint32_t blocks = 0;
-    for (const Run& r : runs) {
-      Bin b{};
-      b.block_begin = blocks;
-      b.row_begin = r.b;
-      b.row_end = r.e;
-      b.kind = r.kind;
-      b.cls = r.cls;
-      b.srow_begin = r.srow;
-      b.seg_begin = static_cast<uint32_t>(segs.size());
-      if (r.kind == KIND_HUB) {
-        for (uint32_t l = r.b; l < r.e; ++l) {
-          HubRow h{l, next_part, 0, r.cls};
-          for (uint64_t e = hrow[l]; e < hrow[l + 1]; e += T.seg)
-            segs.push_back({e, std::min<uint64_t>(e + T.seg, hrow[l + 1]), next_part++, 0});
-          h.part_end = next_part;
-          g->hubs.push_back(h);
-        }
-        blocks += static_cast<uint32_t>(segs.size()) - b.seg_begin;
-      } else if (r.kind == KIND_BLOCK) {
-        blocks += r.e - r.b;
-      } else if (r.kind == KIND_COMBINE) {
-        blocks += (r.e - r.b + BLOCK - 1) / BLOCK;
-      } else {
-        const uint32_t rpb = BLOCK >> r.kind;
-        blocks += (r.e - r.b + rpb - 1) / rpb;
+    for (int cls = 0; cls < 2; ++cls) {
+      const uint32_t r0 = cls ? g->lA : 0, r1 = cls ? lrows : g->lA;
+      if (r1 <= r0) continue;
+      // lanes per row: non-increasing along the (in-degree sorted) rows -> few bins
+      std::vector<uint16_t> kd(r1 - r0);
+      uint16_t run = 0;
+      for (uint32_t l = r1; l-- > r0;) {
+        run = std::max(run, kind_for(hpp[l + 1] - hpp[l], T));
+        kd[l - r0] = run;
       }
-      g->bins.push_back(b);
-      g->bin_edges.push_back(hrow[r.e] - hrow[r.b]);
+      uint32_t i = r0;
+      while (i < r1) {
+        uint32_t e = i + 1;
+        while (e < r1 && kd[e - r0] == kd[i - r0]) ++e;
+        Bin b{};
+        b.block_begin = blocks;
+        b.row_begin = i;
+        b.row_end = e;
+        b.kind = kd[i - r0];
+        b.cls = static_cast<uint16_t>(cls);
+        blocks += b.kind == KIND_BLOCK ? e - i : (e - i + (BLOCK >> b.kind) - 1) / (BLOCK >> b.kind);
+        g->bins.push_back(b);
+        i = e;
+      }
     }
     g->total_blocks = blocks;
     TRY(dmalloc(&g->d_bins, g->bins.size(), err));
     if (!g->bins.empty()) HIPTRY(hipMemcpyAsync(g->d_bins, g->bins.data(), g->bins.size() * sizeof(Bin), hipMemcpyHostToDevice, s));
-    TRY(dmalloc(&g->d_segs, segs.size(), err));
-    if (!segs.empty()) HIPTRY(hipMemcpyAsync(g->d_segs, segs.data(), segs.size() * sizeof(HubSeg), hipMemcpyHostToDevice, s));
   }
-  g->n_parts = next_part;
-  TRY(dmalloc(&g->d_hubs, g->hubs.size(), err));
-  if (!g->hubs.empty()) HIPTRY(hipMemcpyAsync(g->d_hubs, g->hubs.data(), g->hubs.size() * sizeof(HubRow), hipMemcpyHostToDevice, s));
-  TRY(dmalloc(&g->hub_part, next_part, err));
 
   // ---- iteration buffers ----------------------------------------------------------------
   TRY(dmalloc(&g->r_loc[0], lrows, err));
@@ -1290,43 +1375,27 @@ double* dev_x_out(DevGraph* g, int t) { return g->xbuf[(t - 1) & 1]; }
 
 namespace {
 
-// launch helpers for both grids (template dispatch on MODE / NT)
-void launch_rows(const DevGraph* g, StepArgs A, int mode, uint32_t base, uint32_t nblk,
-                 hipStream_t s) {
-  A.block_base = base;
-  const dim3 gr(nblk), bl(BLOCK);
-  if (g->tune.nt) {
-    if (mode == 0) hipLaunchKernelGGL((spmv_round<0, 1>), gr, bl, 0, s, A);
-    else if (mode == 1) hipLaunchKernelGGL((spmv_round<1, 1>), gr, bl, 0, s, A);
-    else hipLaunchKernelGGL((spmv_round<2, 1>), gr, bl, 0, s, A);
-  } else {
-    if (mode == 0) hipLaunchKernelGGL((spmv_round<0, 0>), gr, bl, 0, s, A);
-    else if (mode == 1) hipLaunchKernelGGL((spmv_round<1, 0>), gr, bl, 0, s, A);
-    else hipLaunchKernelGGL((spmv_round<2, 0>), gr, bl, 0, s, A);
-  }
-}
-void launch_slices(const DevGraph* g, StepArgs A, uint32_t t0, uint32_t t1, hipStream_t s) {
-  A.block_base = t0;
-  A.tile_end = t1;
+void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   const bool hot = A.hot_n > 0;
   const size_t lds = hot ? 8ull * A.hot_n : 0;
   // persistent grid: 32 CUs per XCD; one 1024-thread block per CU with the LDS copy of the
-  // hot x prefix, two without it
-  const dim3 gr(NSLICE * 32 * (hot ? 1 : 2)), bl(SLICE_BLOCK);
+  // hot x prefix (PR_STREAM_WG more without it)
+  const int per_cu = hot ? 1 : std::max(1, g->tune.stream_wg);
+  const dim3 gr(NSLICE * 32 * per_cu), bl(STREAM_BLOCK);
   static bool attr_set = false;  // allow the >64 KB dynamic LDS request
   if (hot && !attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_slices<0, true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_stream<0, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_slices<1, true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_stream<1, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   if (g->tune.nt) {
-    if (hot) hipLaunchKernelGGL((spmv_slices<1, true>), gr, bl, lds, s, A);
-    else hipLaunchKernelGGL((spmv_slices<1, false>), gr, bl, 0, s, A);
+    if (hot) hipLaunchKernelGGL((spmv_stream<1, true>), gr, bl, lds, s, A);
+    else hipLaunchKernelGGL((spmv_stream<1, false>), gr, bl, 0, s, A);
   } else {
-    if (hot) hipLaunchKernelGGL((spmv_slices<0, true>), gr, bl, lds, s, A);
-    else hipLaunchKernelGGL((spmv_slices<0, false>), gr, bl, 0, s, A);
+    if (hot) hipLaunchKernelGGL((spmv_stream<0, true>), gr, bl, lds, s, A);
+    else hipLaunchKernelGGL((spmv_stream<0, false>), gr, bl, 0, s, A);
   }
 }
 
@@ -1335,77 +1404,47 @@ void launch_slices(const DevGraph* g, StepArgs A, uint32_t t0, uint32_t t1, hipS
 int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev0,
                       hipEvent_t ev1) {
   std::string* err = nullptr;
-  StepArgs A{};
-  A.row_ptr = g->row_ptr;
-  A.col = g->col;
+  const double* x_in = t == 1 ? g->x_init : g->xbuf[t & 1];
+  StreamArgs S{};
+  S.col = g->col;
+  S.bits = g->bits;
+  S.task_piece = g->task_piece;
+  S.x_in = x_in;
+  S.partial = g->partial;
+  for (int j = 0; j < NSLICE; ++j) {
+    S.sbase[j] = g->sbase[j];
+    S.slen[j] = g->slen[j];
+    S.tbase[j] = g->tbase[j];
+    S.hot_base[j] = g->sm ? (j % g->p) * g->maxA + (j / g->p) * g->SL : 0u;
+  }
+  S.hot_n = g->sm ? std::min(g->tune.hot_lds, g->SL) : 0u;
+  S.colmask = g->tune.colmask;
+  S.dbg = static_cast<uint32_t>(g->tune.dbg);
+  RowArgs A{};
+  A.bins = g->d_bins;
+  A.nbins = static_cast<int>(g->bins.size());
+  A.row_pp = g->row_pp;
+  A.pidx = g->pidx;
+  A.partial = g->partial;
   A.meta = g->meta;
-  A.x_in = t == 1 ? g->x_init : g->xbuf[t & 1];
   A.x_out = dev_x_out(g, t) + static_cast<uint64_t>(g->rank) * g->maxA;
   A.r_old = t == 1 ? nullptr : g->r_loc[(t - 1) & 1];
   A.r_out = g->r_loc[t & 1];
-  A.hub_part = g->hub_part;
-  A.hubs = g->d_hubs;
   A.st = g->state;
   A.shards = g->shards;
-  A.sb = g->sb;
-  A.part = g->part;
-  A.nS = g->nS;
-  A.hub_tiles = g->hub_tiles;
-  A.colmask = g->tune.colmask;
   A.p = static_cast<uint32_t>(g->p);
   A.rank = static_cast<uint32_t>(g->rank);
   A.sm = g->sm ? 1u : 0u;
   A.SL = g->SL;
-  A.hot_n = g->sm ? std::min(g->tune.hot_lds, g->SL) : 0u;
-  for (int j = 0; j < NSLICE; ++j)
-    A.hot_base[j] = g->sm ? (j % g->p) * g->maxA + (j / g->p) * g->SL : 0u;
-  StepArgs AS = A;  // slice launch
-  AS.bins = g->d_sbins;
-  AS.nbins = static_cast<int>(g->sbins.size());
-  AS.segs = g->d_ssegs;
-  A.bins = g->d_bins;
-  A.nbins = static_cast<int>(g->bins.size());
-  A.segs = g->d_segs;
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
-  if (g->tune.split) {
-    // timing mode: one launch per bin, each bracketed by events (DevGraph::split_ms)
-    const size_t nsb = g->sbins.size(), nrb = g->bins.size();
-    if (g->split_ev.empty()) {
-      g->split_ev.resize(2 * (nsb + nrb));
-      for (auto& e : g->split_ev) HIPTRY(hipEventCreate(&e));
-      g->split_ms.assign(nsb + nrb, 0.0);
-    }
-    for (size_t i = 0; i < nsb + nrb; ++i) {
-      const bool sl = i < nsb;
-      const std::vector<Bin>& bv = sl ? g->sbins : g->bins;
-      const size_t k = sl ? i : i - nsb;
-      const uint32_t tot = sl ? g->slice_tiles : g->total_blocks;
-      const uint32_t b0 = bv[k].block_begin;
-      const uint32_t b1 = k + 1 < bv.size() ? bv[k + 1].block_begin : tot;
-      HIPTRY(hipEventRecord(g->split_ev[2 * i], s));
-      if (b1 > b0) {
-        if (sl) launch_slices(g, AS, b0, b1, s);
-        else launch_rows(g, A, mode, b0, b1 - b0, s);
-      }
-      HIPTRY(hipEventRecord(g->split_ev[2 * i + 1], s));
-    }
-    HIPTRY(hipStreamSynchronize(s));
-    for (size_t i = 0; i < nsb + nrb; ++i) {
-      float ms = 0.f;
-      HIPTRY(hipEventElapsedTime(&ms, g->split_ev[2 * i], g->split_ev[2 * i + 1]));
-      g->split_ms[i] += ms;
-    }
-  } else {
-    if (g->slice_tiles) launch_slices(g, AS, 0, g->slice_tiles, s);
-    if (g->total_blocks) launch_rows(g, A, mode, 0, g->total_blocks, s);
+  if (g->tbase[NSLICE]) launch_stream(g, S, s);
+  if (g->total_blocks) {
+    const dim3 gr(g->total_blocks), bl(BLOCK);
+    if (mode == 0) hipLaunchKernelGGL(spmv_rows<0>, gr, bl, 0, s, A);
+    else if (mode == 1) hipLaunchKernelGGL(spmv_rows<1>, gr, bl, 0, s, A);
+    else hipLaunchKernelGGL(spmv_rows<2>, gr, bl, 0, s, A);
   }
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
-  if (!g->hubs.empty()) {
-    const uint32_t nh = static_cast<uint32_t>(g->hubs.size());
-    if (mode == 0) hipLaunchKernelGGL(hub_round<0>, dim3(nh), dim3(BLOCK), 0, s, A);
-    else if (mode == 1) hipLaunchKernelGGL(hub_round<1>, dim3(nh), dim3(BLOCK), 0, s, A);
-    else hipLaunchKernelGGL(hub_round<2>, dim3(nh), dim3(BLOCK), 0, s, A);
-  }
   hipLaunchKernelGGL(reduce_shards, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local);
   HIPTRY(hipGetLastError());
   return PR_OK;
@@ -1434,4 +1473,49 @@ int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s) {
   return PR_OK;
 }
 
+
+int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s, std::string* err) {
+  const Layout L = layout_of(g);
+  StreamPos SP{};
+  uint64_t acc = 0;
+  for (int j = 0; j < NSLICE; ++j) {
+    SP.start[j] = acc;
+    acc += g->slen[j];
+    SP.sbase[j] = g->sbase[j];
+    SP.tbase[j] = g->tbase[j];
+  }
+  SP.start[NSLICE] = acc;
+  SP.tbase[NSLICE] = g->tbase[NSLICE];
+  const uint64_t m = g->lnnz;
+  Temp tmp;
+  uint32_t* prow = nullptr;
+  uint64_t *k0 = nullptr, *k1 = nullptr, *rp = nullptr;
+  uint32_t* c = nullptr;
+  struct Free {
+    std::vector<void*> v;
+    ~Free() { for (void* p : v) if (p) (void)hipFree(p); }
+  } fr;
+  TRY(dmalloc(&prow, g->n_pieces, err)); fr.v.push_back(prow);
+  TRY(dmalloc(&k0, m, err)); fr.v.push_back(k0);
+  TRY(dmalloc(&k1, m, err)); fr.v.push_back(k1);
+  TRY(dmalloc(&rp, g->lrows + 1ull, err)); fr.v.push_back(rp);
+  TRY(dmalloc(&c, m, err)); fr.v.push_back(c);
+  if (g->lrows) hipLaunchKernelGGL(k_piece_row_of, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->row_pp, g->pidx, g->lrows, prow);
+  if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_for(g->stream_len)), dim3(BLOCK), 0, s, g->col, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, SP, g->stream_len, k0);
+  rocprim::double_buffer<uint64_t> db(k0, k1);
+  size_t tb = 0;
+  HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, m, 0, 64, s));
+  TRY(tmp.ensure(tb, err));
+  if (m) HIPTRY(rocprim::radix_sort_keys(tmp.p, tb, db, m, 0, 64, s));
+  HIPTRY(hipMemsetAsync(rp, 0, 8ull * (g->lrows + 1), s));
+  if (m) hipLaunchKernelGGL(k_export_split, dim3(grid_for(m)), dim3(BLOCK), 0, s, db.current(), m, c, rp);
+  HIPTRY(hipGetLastError());
+  if (row_ptr) HIPTRY(hipMemcpyAsync(row_ptr, rp, 8ull * g->lrows, hipMemcpyDeviceToHost, s));
+  if (col && m) HIPTRY(hipMemcpyAsync(col, c, 4ull * m, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipStreamSynchronize(s));
+  if (row_ptr) row_ptr[g->lrows] = m;
+  return PR_OK;
+}
+
 }  // namespace prmi
+

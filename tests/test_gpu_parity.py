@@ -245,7 +245,10 @@ def test_pagerank_main_cli_contract(P, O, tmp_path):
 
 # ---- multi-rank layout on one GPU: single-process rank group (copies replace RCCL) -------
 @pytest.mark.parametrize("p", [2, 3, 4, 8])
-def test_rank_group_bit_identical_to_single(P, p):
+def test_rank_group_matches_single(P, O, p):
+    """p ranks (rows dealt in 16-row chunks, x exchanged every round) against one rank and
+    the oracle.  Each rank's stream cuts rows into pieces at its own task boundaries, so the
+    summation order (and the last bits) may differ from p = 1; the defined set may not."""
     ref = P.Engine()
     ref.generate_rmat(15, 16, 6)
     ref.run(10)
@@ -257,8 +260,14 @@ def test_rank_group_bit_identical_to_single(P, p):
     assert sum(i["local_rows"] for i in info) == info[0]["n_rows"]
     grp.run(10)
     rp = grp.members[p - 1].ranks()
-    assert np.array_equal(r1.view(np.uint64), rp.view(np.uint64))
-    assert grp.members[0].topk(100) == ref.topk(100)
+    assert parity.assert_ranks_close(rp, r1, rtol=1e-12) <= 1e-12
+    exp = O.Graph.from_rmat(15, 16, 6).run(10)["ranks"]
+    parity.assert_ranks_close(rp, exp)
+    grp.run(10)   # deterministic for a fixed rank count
+    assert np.array_equal(rp.view(np.uint64), grp.members[0].ranks().view(np.uint64))
+    top_ref = [(str(v).encode(), r) for _, v, r in ref.topk(100)]
+    top_grp = [(str(v).encode(), r) for _, v, r in grp.members[0].topk(100)]
+    parity.assert_same_order_mod_ties(top_grp, top_ref, rtol=1e-12)
     grp.close()
 
 
