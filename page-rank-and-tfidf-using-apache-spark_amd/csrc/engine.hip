@@ -353,9 +353,13 @@ struct StreamArgs {
   uint32_t hot_n;            // x entries per slice served from LDS
   uint32_t colmask;          // PR_COLMASK (timing experiments only)
   uint32_t dbg;              // PR_DBG timing experiments: 1 no stores, 2 no gathers, 4 no starts
+  uint32_t x_bytes;          // bytes of x (< 2^31: the buffer-load range check drops hot lanes)
 };
 constexpr int STREAM_BLOCK = 1024;
+constexpr int STG = 128;           // per-wave LDS staging window for piece stores (doubles)
+constexpr uint32_t HOT_MAX = 20480 - (STREAM_BLOCK / 64) * STG;  // LDS left for the hot x copy
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <int NT, bool HOT>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
@@ -372,6 +376,9 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     for (uint32_t i = threadIdx.x; i < H; i += blockDim.x) hot[i] = x[base + i];
     __syncthreads();
   }
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(x), static_cast<short>(0),
+                                        static_cast<int>(A.x_bytes), 0x00020000);
   const uint64_t len = A.slen[j];
   const uint32_t ntask = static_cast<uint32_t>((len + TASK - 1) / TASK);
   const uint32_t* __restrict__ colj = A.col + A.sbase[j];
@@ -406,9 +413,9 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     if (A.dbg & 4u) b = 0;
     if (lane == 0) b |= 1u;                       // a task always starts a piece
     b &= nv >= EPL ? 0xFFFFu : ((1u << nv) - 1u);  // no starts past the stream end
-    // Sixteen gathers issued back to back, no branches: a hot source reads its LDS copy and
-    // points its (then redundant) global load at the slice's first entry, which every hot
-    // lane of the instruction shares (one request); padding edges read x[0] and are masked.
+    // Sixteen gathers issued back to back, no branches: a hot source reads its LDS copy, and
+    // its lane of the buffer load gets an out-of-range offset, which the range check drops
+    // before any memory request; padding edges read x[0] and are masked below.
     double v[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
@@ -419,8 +426,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
         const uint32_t o = q - base;
         const bool h = o < H;
         const double lv = hot[h ? o : 0u];
-        const double gv = x[h ? base : q];
-        v[k] = h ? lv : gv;
+        const u32x2 g2 = __builtin_amdgcn_raw_buffer_load_b64(xr, h ? 0x80000000u : q * 8u, 0, 0);
+        v[k] = h ? lv : __builtin_bit_cast(double, g2);
       } else {
         v[k] = x[q];
       }
@@ -438,22 +445,21 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       const int y = __shfl_up(C, d);
       if (lane >= d) C += y;
     }
-    uint32_t pc = tp0 + static_cast<uint32_t>(C - cnt) - 1u;  // piece open before edge 0
-    // pass over the lane's edges: pieces complete inside the lane are written here
+    const uint32_t first = static_cast<uint32_t>(C - cnt);  // task-relative index of the lane's first start
+    const uint32_t total = static_cast<uint32_t>(__shfl(C, 63));  // pieces of the task
+    // the lane's head (edges before its first start) and its open piece
     double run = 0.0, head = 0.0;
-    bool in_head = (b & 1u) == 0u;
+    {
+      bool ih = (b & 1u) == 0u;
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      if ((b >> k) & 1u) {
-        if (k > 0) {
-          if (in_head) head = run;
-          else if (!(A.dbg & 1u)) part[pc] = run;
-          in_head = false;
+      for (int k = 0; k < EPL; ++k) {
+        if ((b >> k) & 1u) {
+          if (k > 0 && ih) head = run;
+          ih = false;
+          run = 0.0;
         }
-        ++pc;
-        run = 0.0;
+        run += v[k];
       }
-      run += v[k];
     }
     // segmented inclusive scan of the open piece over lanes (flag: lane holds a start)
     double S = run;
@@ -471,13 +477,45 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     const uint32_t bn = __shfl_down(b, 1);
     const int nvn = __shfl_down(nv, 1);
     const bool closes = lane == 63 || nvn == 0 || (bn & 1u) != 0u;  // next edge starts a piece
-    if (nv > 0 && !(A.dbg & 1u)) {
-      if (b == 0u) {
-        if (closes) part[pc] = S;                     // lane inside a longer piece
-      } else {
-        if (!(b & 1u)) part[tp0 + static_cast<uint32_t>(C - cnt) - 1u] = carry + head;
-        if (closes) part[pc] = run;                   // the lane's last piece
+    // Pieces go to the wave's LDS staging window (STG pieces at a time) and leave it as
+    // contiguous 512-byte stores: one L2 request per line instead of one per piece.
+    double* stg = hot + H + (threadIdx.x >> 6) * STG;
+    for (uint32_t w0 = 0; w0 < total; w0 += STG) {
+      const uint32_t wn = min(total - w0, static_cast<uint32_t>(STG));
+      auto put = [&](uint32_t r, double val) {
+        if (r - w0 < wn) stg[r - w0] = val;
+      };
+      if (nv > 0 && first + cnt > w0 && first < w0 + wn + 1u) {
+        uint32_t r = first - 1u;  // relative index of the piece open before edge 0
+        double rr = 0.0;
+        bool ih = (b & 1u) == 0u;
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) {
+          if ((b >> k) & 1u) {
+            if (k > 0) {
+              if (!ih) put(r, rr);  // a piece that starts and ends inside the lane
+              ih = false;
+            }
+            ++r;
+            rr = 0.0;
+          }
+          rr += v[k];
+        }
+        if (b == 0u) {
+          if (closes) put(first - 1u, S);            // lane inside a longer piece
+        } else {
+          if (!(b & 1u)) put(first - 1u, carry + head);
+          if (closes) put(static_cast<uint32_t>(C) - 1u, run);  // the lane's last piece
+        }
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (!(A.dbg & 1u))
+        for (uint32_t i = lane; i < wn; i += 64) part[tp0 + w0 + i] = stg[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
 }
@@ -1377,25 +1415,26 @@ namespace {
 
 void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   const bool hot = A.hot_n > 0;
-  const size_t lds = hot ? 8ull * A.hot_n : 0;
+  const size_t lds = 8ull * (A.hot_n + (STREAM_BLOCK / 64) * STG);
   // persistent grid: 32 CUs per XCD; one 1024-thread block per CU with the LDS copy of the
   // hot x prefix (PR_STREAM_WG more without it)
   const int per_cu = hot ? 1 : std::max(1, g->tune.stream_wg);
   const dim3 gr(NSLICE * 32 * per_cu), bl(STREAM_BLOCK);
   static bool attr_set = false;  // allow the >64 KB dynamic LDS request
-  if (hot && !attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_stream<0, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_stream<1, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (!attr_set) {
+    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<0, true>),
+                          reinterpret_cast<const void*>(&spmv_stream<1, true>),
+                          reinterpret_cast<const void*>(&spmv_stream<0, false>),
+                          reinterpret_cast<const void*>(&spmv_stream<1, false>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   if (g->tune.nt) {
     if (hot) hipLaunchKernelGGL((spmv_stream<1, true>), gr, bl, lds, s, A);
-    else hipLaunchKernelGGL((spmv_stream<1, false>), gr, bl, 0, s, A);
+    else hipLaunchKernelGGL((spmv_stream<1, false>), gr, bl, lds, s, A);
   } else {
     if (hot) hipLaunchKernelGGL((spmv_stream<0, true>), gr, bl, lds, s, A);
-    else hipLaunchKernelGGL((spmv_stream<0, false>), gr, bl, 0, s, A);
+    else hipLaunchKernelGGL((spmv_stream<0, false>), gr, bl, lds, s, A);
   }
 }
 
@@ -1417,7 +1456,9 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
     S.tbase[j] = g->tbase[j];
     S.hot_base[j] = g->sm ? (j % g->p) * g->maxA + (j / g->p) * g->SL : 0u;
   }
-  S.hot_n = g->sm ? std::min(g->tune.hot_lds, g->SL) : 0u;
+  // the LDS path addresses x through a buffer descriptor: byte offsets must stay below 2^31
+  S.hot_n = g->sm && g->X < (1ull << 28) ? std::min({g->tune.hot_lds, g->SL, HOT_MAX}) : 0u;
+  S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   S.colmask = g->tune.colmask;
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   RowArgs A{};
