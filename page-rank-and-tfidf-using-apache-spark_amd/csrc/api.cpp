@@ -94,7 +94,7 @@ int build_device(pr_ctx* c, const prmi::BuildInput& in) {
             c->opts.rank, c->dg.ms_build, c->dg.n, (unsigned long long)c->dg.nnz, c->dg.R,
             c->dg.lrows, (unsigned long long)c->dg.lnnz, c->dg.nseg,
             (unsigned long long)c->dg.n_pairs, (unsigned long long)c->dg.n_pieces,
-            c->dg.tbase[prmi::NSLICE], c->dg.bins.size(), c->dg.total_blocks);
+            c->dg.ntask, c->dg.bins.size(), c->dg.total_blocks);
   return PR_OK;
 }
 

@@ -62,10 +62,11 @@ struct IterState {
 struct Tuning {
   int epl = 4;          // row kernel: target pieces per lane
   uint32_t kb = 1024;   // row kernel: piece count above which one workgroup takes a row
-  uint32_t qh = 458752; // PR_QH: hot segment length per slice (x entries, 3.5 MiB)
+  uint32_t qh = 458752; // PR_QH: L2-hot segment length per slice after the LDS blocks (3.5 MiB)
+  int nlds = 8;         // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
-  int nt = 1;           // PR_NT: non-temporal loads for the streamed arrays
-  uint32_t hot_lds = 20480;  // PR_HOTLDS: x entries of each slice region copied to LDS (<=20480)
+  int nt = 0;           // PR_NT: non-temporal loads for the streamed arrays (slower: 3.8 vs 6 TB/s)
+  uint32_t hot_lds = 20480;  // PR_HOTLDS: LDS block length (x entries, capped by the staging room)
   uint32_t colmask = 0xFFFFFFFFu;  // PR_COLMASK: timing-only gather working-set restriction
   int dbg = 0;          // PR_DBG: timing-only experiments in the stream kernel (see StreamArgs)
   int stream_wg = 1;    // PR_STREAM_WG: stream workgroups per CU (1 with the LDS copy)
@@ -87,10 +88,16 @@ struct DevGraph {
   uint64_t n_dang_entries = 0;
   uint64_t digest[2] = {0, 0};
   double ms_build = 0;
-  // slice streams: slice j's edges at [sbase[j], sbase[j] + slen[j]) of col / bits
-  uint64_t sbase[NSLICE] = {}, slen[NSLICE] = {};
-  uint32_t tbase[NSLICE + 1] = {};  // first global task of slice j (tbase[8] = all tasks)
-  uint32_t nseg = 0;              // segments per slice (hot + cold)
+  // slice streams: group gr = slice * (nlds + 1) + (LDS block, or nlds = the L2 part) owns
+  // tasks [gtask[gr], gtask[gr+1]) = stream positions gtask*TASK.. and sorted-key edges
+  // [gstart[gr], gstart[gr+1]) (a group's tail task is padded with PAD_COL edges)
+  std::vector<uint32_t> gtask;
+  std::vector<uint64_t> gstart;
+  uint32_t* d_gtask = nullptr;
+  uint64_t* d_gstart = nullptr;
+  uint32_t ntask = 0;
+  uint32_t nlds = 0, hot_h = 0;   // LDS blocks per slice and their length (x entries)
+  uint32_t nseg = 0;              // segments per slice (LDS blocks + L2-hot + cold)
   uint64_t n_pieces = 0, n_pairs = 0;
   uint64_t stream_len = 0;        // padded length of col (multiple of TASK)
   // device arrays

@@ -297,7 +297,7 @@ __device__ __forceinline__ void group_tile(const RowArgs& A, double a, const Bin
   const bool active = row < b.row_end;
   double s = 0.0;
   if (active)
-    s = strided_sum<G, 1>(A.pidx, GatherX{A.partial}, A.row_pp[row], A.row_pp[row + 1], gl);
+    s = strided_sum<G, 0>(A.pidx, GatherX{A.partial}, A.row_pp[row], A.row_pp[row + 1], gl);
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
   row_epilogue<MODE>(A, a, b.cls, row, s, active && gl == 0, lds);
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     case 6: group_tile<64, MODE>(A, a, bin, blk, lds); break;
     default: {  // KIND_BLOCK: one workgroup per row
       const uint32_t row = bin.row_begin + blk;
-      double s = strided_sum<BLOCK, 1>(A.pidx, GatherX{A.partial}, A.row_pp[row],
+      double s = strided_sum<BLOCK, 0>(A.pidx, GatherX{A.partial}, A.row_pp[row],
                                        A.row_pp[row + 1], threadIdx.x);
       s = block_sum(s, red);
       row_epilogue<MODE>(A, a, bin.cls, row, s, threadIdx.x == 0, lds);
@@ -344,24 +344,66 @@ struct StreamArgs {
   const uint32_t* col;
   const uint16_t* bits;
   const uint32_t* task_piece;
+  const uint32_t* gtask;     // [8 * (nlds + 1) + 1] first task of each stream group
   const double* x_in;
   double* partial;
-  uint64_t sbase[NSLICE];    // first stream edge of slice j (multiple of TASK)
-  uint64_t slen[NSLICE];     // edges of slice j
-  uint32_t tbase[NSLICE];    // first global task of slice j
   uint32_t hot_base[NSLICE]; // x position of each slice region's start
-  uint32_t hot_n;            // x entries per slice served from LDS
+  uint32_t nlds, H;          // LDS blocks per slice, entries per block
   uint32_t colmask;          // PR_COLMASK (timing experiments only)
   uint32_t dbg;              // PR_DBG timing experiments: 1 no stores, 2 no gathers, 4 no starts
-  uint32_t x_bytes;          // bytes of x (< 2^31: the buffer-load range check drops hot lanes)
+  uint32_t x_bytes;          // bytes of x (< 2^31: the buffer-load range check drops LDS lanes
+                             // and PAD_COL padding)
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 128;           // per-wave LDS staging window for piece stores (doubles)
-constexpr uint32_t HOT_MAX = 20480 - (STREAM_BLOCK / 64) * STG;  // LDS left for the hot x copy
+constexpr uint32_t HOT_MAX = 20480 - (STREAM_BLOCK / 64) * STG;  // LDS left for the x block
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-template <int NT, bool HOT>
+// Sixteen exec-masked buffer gathers x[off/8] into v[k] (lanes outside gm[k] keep v[k]),
+// then one s_waitcnt: the asm block ends with its loads landed, so the compiler never sees
+// an in-flight destination.
+__device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[EPL],
+                                         const uint64_t (&gm)[EPL], __amdgpu_buffer_rsrc_t xr) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n"
+      "s_and_b64 exec, %[sv], %[m0]\n  buffer_load_dwordx2 %[d0], %[o0], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m1]\n  buffer_load_dwordx2 %[d1], %[o1], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m2]\n  buffer_load_dwordx2 %[d2], %[o2], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m3]\n  buffer_load_dwordx2 %[d3], %[o3], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m4]\n  buffer_load_dwordx2 %[d4], %[o4], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m5]\n  buffer_load_dwordx2 %[d5], %[o5], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m6]\n  buffer_load_dwordx2 %[d6], %[o6], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m7]\n  buffer_load_dwordx2 %[d7], %[o7], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m8]\n  buffer_load_dwordx2 %[d8], %[o8], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m9]\n  buffer_load_dwordx2 %[d9], %[o9], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m10]\n buffer_load_dwordx2 %[d10], %[o10], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m11]\n buffer_load_dwordx2 %[d11], %[o11], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m12]\n buffer_load_dwordx2 %[d12], %[o12], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m13]\n buffer_load_dwordx2 %[d13], %[o13], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m14]\n buffer_load_dwordx2 %[d14], %[o14], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m15]\n buffer_load_dwordx2 %[d15], %[o15], %[rs], 0 offen\n"
+      "s_mov_b64 exec, %[sv]\n"
+      "s_waitcnt vmcnt(0)\n"
+      : [d0] "+v"(v[0]), [d1] "+v"(v[1]), [d2] "+v"(v[2]), [d3] "+v"(v[3]),
+        [d4] "+v"(v[4]), [d5] "+v"(v[5]), [d6] "+v"(v[6]), [d7] "+v"(v[7]),
+        [d8] "+v"(v[8]), [d9] "+v"(v[9]), [d10] "+v"(v[10]), [d11] "+v"(v[11]),
+        [d12] "+v"(v[12]), [d13] "+v"(v[13]), [d14] "+v"(v[14]), [d15] "+v"(v[15]),
+        [sv] "=&s"(sv)
+      : [o0] "v"(qo[0]), [o1] "v"(qo[1]), [o2] "v"(qo[2]), [o3] "v"(qo[3]),
+        [o4] "v"(qo[4]), [o5] "v"(qo[5]), [o6] "v"(qo[6]), [o7] "v"(qo[7]),
+        [o8] "v"(qo[8]), [o9] "v"(qo[9]), [o10] "v"(qo[10]), [o11] "v"(qo[11]),
+        [o12] "v"(qo[12]), [o13] "v"(qo[13]), [o14] "v"(qo[14]), [o15] "v"(qo[15]),
+        [m0] "s"(gm[0]), [m1] "s"(gm[1]), [m2] "s"(gm[2]), [m3] "s"(gm[3]),
+        [m4] "s"(gm[4]), [m5] "s"(gm[5]), [m6] "s"(gm[6]), [m7] "s"(gm[7]),
+        [m8] "s"(gm[8]), [m9] "s"(gm[9]), [m10] "s"(gm[10]), [m11] "s"(gm[11]),
+        [m12] "s"(gm[12]), [m13] "s"(gm[13]), [m14] "s"(gm[14]), [m15] "s"(gm[15]),
+        [rs] "s"(xr)
+      : "memory");
+}
+
+template <int NT>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
   const uint32_t j = blockIdx.x % NSLICE;
@@ -369,74 +411,93 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   const int lane = threadIdx.x & 63;
   const uint32_t w = (blockIdx.x / NSLICE) * wpb + (threadIdx.x >> 6);
   const uint32_t nw = (gridDim.x / NSLICE) * wpb;
-  const uint32_t base = A.hot_base[j];
-  const uint32_t H = HOT ? A.hot_n : 0u;
   const double* __restrict__ x = A.x_in;
-  if constexpr (HOT) {
-    for (uint32_t i = threadIdx.x; i < H; i += blockDim.x) hot[i] = x[base + i];
-    __syncthreads();
-  }
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(x), static_cast<short>(0),
                                         static_cast<int>(A.x_bytes), 0x00020000);
-  const uint64_t len = A.slen[j];
-  const uint32_t ntask = static_cast<uint32_t>((len + TASK - 1) / TASK);
-  const uint32_t* __restrict__ colj = A.col + A.sbase[j];
-  const uint16_t* __restrict__ bitsj = A.bits + A.sbase[j] / EPL;
-  const uint32_t* __restrict__ tpj = A.task_piece + A.tbase[j];
+  const uint32_t* __restrict__ col = A.col;
+  const uint16_t* __restrict__ bits = A.bits;
+  const uint32_t* __restrict__ tpa = A.task_piece;
   double* __restrict__ part = A.partial;
   const uint32_t cm = A.colmask;
+  const uint32_t ngs = A.nlds + 1;
+  double* stg = hot + A.H * (A.nlds ? 1u : 0u) + (threadIdx.x >> 6) * STG;
   // software pipeline: the next task's stream words are in flight while this task gathers
   u32x4 cn[4];
   uint32_t bnx = 0, tpn = 0;
   auto fetch = [&](uint32_t tt) {
     const uint64_t o = static_cast<uint64_t>(tt) * TASK + lane * EPL;
-    // the stream buffer is padded to whole tasks: these loads never leave it
-    const u32x4* cp = reinterpret_cast<const u32x4*>(colj + o);
+    // groups are padded to whole tasks: these loads never leave the stream buffer
+    const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
 #pragma unroll
     for (int q = 0; q < 4; ++q) cn[q] = ld_stream<NT>(cp + q);
-    bnx = ld_stream<NT>(bitsj + o / EPL);
-    tpn = tpj[tt];
+    bnx = ld_stream<NT>(bits + o / EPL);
+    tpn = tpa[tt];
   };
-  if (w < ntask) fetch(w);
-  for (uint32_t t = w; t < ntask; t += nw) {
-    const uint64_t off = static_cast<uint64_t>(t) * TASK;
-    const uint64_t rem = len - off;
-    const int nval = rem >= static_cast<uint64_t>(TASK) ? TASK : static_cast<int>(rem);
-    const int lo = lane * EPL;
-    const int nv = min(max(nval - lo, 0), EPL);
-    u32x4 cv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cv[q] = cn[q];
-    uint32_t b = bnx;
-    const uint32_t tp0 = tpn;
-    if (A.dbg & 4u) b = 0;
-    if (lane == 0) b |= 1u;                       // a task always starts a piece
-    b &= nv >= EPL ? 0xFFFFu : ((1u << nv) - 1u);  // no starts past the stream end
-    // Sixteen gathers issued back to back, no branches: a hot source reads its LDS copy, and
-    // its lane of the buffer load gets an out-of-range offset, which the range check drops
-    // before any memory request; padding edges read x[0] and are masked below.
-    double v[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      const uint32_t q = cv[k >> 2][k & 3] & cm;
-      if (A.dbg & 2u) {
-        v[k] = static_cast<double>(q);
-      } else if constexpr (HOT) {
-        const uint32_t o = q - base;
-        const bool h = o < H;
-        const double lv = hot[h ? o : 0u];
-        const u32x2 g2 = __builtin_amdgcn_raw_buffer_load_b64(xr, h ? 0x80000000u : q * 8u, 0, 0);
-        v[k] = h ? lv : __builtin_bit_cast(double, g2);
-      } else {
-        v[k] = x[q];
-      }
+  // the slice's groups in order: LDS blocks 0..nlds-1 (each with its own LDS fill), then
+  // the L2 part (no LDS block)
+  // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
+  // with 1/nlds of the L2 part's tasks (LDS-bound and L2-bound work side by side); with no
+  // LDS blocks the single phase is the whole stream.
+  const uint32_t l2b = A.gtask[j * ngs + A.nlds], l2e = A.gtask[j * ngs + A.nlds + 1];
+  const uint32_t nph = A.nlds ? A.nlds : 1u;
+  for (uint32_t gi = 0; gi < nph; ++gi) {
+    uint32_t tb = l2b, te = l2b, rb = l2b, re = l2e;  // LDS-block tasks, L2 share
+    uint32_t hb = 0, Hs = 0;
+    if (A.nlds) {
+      tb = A.gtask[j * ngs + gi];
+      te = A.gtask[j * ngs + gi + 1];
+      rb = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * gi) / A.nlds);
+      re = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * (gi + 1)) / A.nlds);
+      hb = A.hot_base[j] + gi * A.H;
+      Hs = A.H;
+      __syncthreads();  // every wave is done with the previous block
+      if (te > tb)
+        for (uint32_t i = threadIdx.x; i < Hs; i += blockDim.x) hot[i] = x[hb + i];
+      __syncthreads();
     }
-    // next task's stream words, issued after the gathers so that waiting for the gathers
-    // (vmcnt counts in issue order) leaves them in flight
-    fetch(min(t + nw, ntask - 1));
+    const uint32_t nL = te - tb, nR = re - rb, nm = min(nL, nR);
+    // virtual index u -> task: alternate LDS / L2 tasks while both last, then the rest
+    auto task_of = [&](uint32_t u) -> uint32_t {
+      if (u < 2 * nm) return (u & 1u) ? rb + (u >> 1) : tb + (u >> 1);
+      return nL > nR ? tb + (u - nm) : rb + (u - nm);
+    };
+    const uint32_t nu = nL + nR;
+    if (w < nu) fetch(task_of(w));
+    for (uint32_t u = w; u < nu; u += nw) {
+      const uint32_t t = task_of(u);
+      (void)t;
+      u32x4 cv[4];
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) v[k] = k < nv ? v[k] : 0.0;
+      for (int q = 0; q < 4; ++q) cv[q] = cn[q];
+      uint32_t b = bnx;
+      const uint32_t tp0 = tpn;
+      if (A.dbg & 4u) b = 0;
+      if (lane == 0) b |= 1u;  // a task always starts a piece
+      // next task's stream words first: they stay in flight while this task gathers
+      if (u + nw < nu) fetch(task_of(u + nw));
+      // Sixteen gathers: a source inside the LDS block reads the LDS copy; the others are
+      // buffer loads issued back to back with EXEC cut to the lanes that need them (the
+      // address unit then spends no cycles on LDS lanes), then one wait for all of them.
+      // PAD_COL lanes fall outside the buffer range and read 0.
+      double v[EPL];
+      uint32_t qo[EPL];
+      uint64_t gm[EPL];
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        const uint32_t q = cv[k >> 2][k & 3] & cm;
+        const uint32_t o = q - hb;
+        const bool h = o < Hs;
+        v[k] = hot[h ? o : 0u];
+        qo[k] = q * 8u;
+        gm[k] = __ballot(!h);
+      }
+      if (A.dbg & 2u) {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) v[k] = static_cast<double>(qo[k] & 0xFFFF);
+      } else {
+        gather16(v, qo, gm, xr);
+      }
     // exclusive prefix (over lanes) of the piece starts -> first piece index of this lane
     const int cnt = __popc(b);
     int C = cnt;
@@ -463,7 +524,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     }
     // segmented inclusive scan of the open piece over lanes (flag: lane holds a start)
     double S = run;
-    bool F = b != 0u || nv == 0;
+    bool F = b != 0u;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const double Su = __shfl_up(S, d);
@@ -475,17 +536,15 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     }
     const double carry = __shfl_up(S, 1);
     const uint32_t bn = __shfl_down(b, 1);
-    const int nvn = __shfl_down(nv, 1);
-    const bool closes = lane == 63 || nvn == 0 || (bn & 1u) != 0u;  // next edge starts a piece
+    const bool closes = lane == 63 || (bn & 1u) != 0u;  // next edge starts a piece
     // Pieces go to the wave's LDS staging window (STG pieces at a time) and leave it as
     // contiguous 512-byte stores: one L2 request per line instead of one per piece.
-    double* stg = hot + H + (threadIdx.x >> 6) * STG;
     for (uint32_t w0 = 0; w0 < total; w0 += STG) {
       const uint32_t wn = min(total - w0, static_cast<uint32_t>(STG));
       auto put = [&](uint32_t r, double val) {
         if (r - w0 < wn) stg[r - w0] = val;
       };
-      if (nv > 0 && first + cnt > w0 && first < w0 + wn + 1u) {
+      if (first + cnt > w0 && first < w0 + wn + 1u) {
         uint32_t r = first - 1u;  // relative index of the piece open before edge 0
         double rr = 0.0;
         bool ih = (b & 1u) == 0u;
@@ -516,6 +575,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     }
   }
 }
@@ -735,9 +795,14 @@ __global__ void k_x_init(const uint32_t* perm, const uint32_t* outdeg, uint32_t 
 
 // ---- slice streams -----------------------------------------------------------------------
 // q-space of a slice: class-A columns [0, SLq) in hotness order, then class-C columns.
+// Segments of q: nlds LDS blocks of H entries, the L2-hot range of QL entries, then cold
+// ranges of S entries.  Stream groups per slice: one per LDS block + one for everything
+// after it; every group starts on a task boundary (padding: col = PAD, gathers read 0).
+constexpr uint32_t PAD_COL = 0xFFFFFFFFu;
 struct StreamGeo {
   uint32_t SLq;       // q-space length of the class-A part of one slice
-  uint32_t QH, S;     // hot segment length, cold segment length (x entries)
+  uint32_t nlds, H;   // LDS blocks per slice and their length
+  uint32_t QL, S;     // L2-hot range length, cold segment length (x entries)
   int qb, rb, sgb;    // key fields: q within segment | local row | segment | slice
 };
 __device__ __forceinline__ void col_slice_q(const Layout& L, const StreamGeo& G, uint32_t k,
@@ -757,6 +822,30 @@ __device__ __forceinline__ uint32_t col_of_slice_q(const Layout& L, const Stream
   if (q < G.SLq) return ((q / CHUNK) * NSLICE + sl) * CHUNK + q % CHUNK;
   const uint32_t qc = q - G.SLq;
   return L.R + ((qc / CHUNK) * NSLICE + sl) * CHUNK + qc % CHUNK;
+}
+__device__ __forceinline__ void seg_of_q(const StreamGeo& G, uint32_t q, uint32_t& seg,
+                                         uint32_t& qin) {
+  const uint32_t ql = G.nlds * G.H;
+  if (q < ql) {
+    seg = q / G.H;
+    qin = q % G.H;
+  } else if (q - ql < G.QL) {
+    seg = G.nlds;
+    qin = q - ql;
+  } else {
+    seg = G.nlds + 1 + (q - ql - G.QL) / G.S;
+    qin = (q - ql - G.QL) % G.S;
+  }
+}
+__device__ __forceinline__ uint32_t q_of_seg(const StreamGeo& G, uint32_t seg, uint32_t qin) {
+  if (seg < G.nlds) return seg * G.H + qin;
+  if (seg == G.nlds) return G.nlds * G.H + qin;
+  return G.nlds * G.H + G.QL + (seg - G.nlds - 1) * G.S + qin;
+}
+__device__ __forceinline__ uint32_t group_of_key(const StreamGeo& G, uint64_t k) {
+  const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
+  const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
+  return sl * (G.nlds + 1) + min(seg, G.nlds);
 }
 // internal column id of an x position (inverse of xpos)
 __device__ __forceinline__ uint32_t col_of_xpos(const Layout& L, uint32_t x) {
@@ -785,10 +874,9 @@ __global__ void k_stream_keys(const uint64_t* uk, uint64_t nnz, int nb, const ui
     const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
     const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
     keep = owner_of(L, kd) == L.rank;
-    uint32_t sl, q;
+    uint32_t sl, q, seg, qin;
     col_slice_q(L, G, ks, sl, q);
-    const uint32_t seg = q < G.QH ? 0u : 1u + (q - G.QH) / G.S;
-    const uint32_t qin = seg ? (q - G.QH) % G.S : q;
+    seg_of_q(G, q, seg, qin);
     key = (static_cast<uint64_t>(sl) << (G.sgb + G.rb + G.qb)) |
           (static_cast<uint64_t>(seg) << (G.rb + G.qb)) |
           (static_cast<uint64_t>(local_of(L, kd)) << G.qb) | qin;
@@ -807,43 +895,31 @@ __global__ void k_stream_keys(const uint64_t* uk, uint64_t nnz, int nb, const ui
   if (keep) out[base + __popcll(mask & ((1ull << lane) - 1))] = key;
 }
 
-// first sorted edge of each slice (atomicMin; slices without edges keep the sentinel)
-__global__ void k_slice_starts(const uint64_t* key, uint64_t n, int shift,
+// first sorted edge of each stream group (atomicMin; empty groups keep the sentinel)
+__global__ void k_group_starts(const uint64_t* key, uint64_t n, StreamGeo G,
                                unsigned long long* starts) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   if (e >= n) return;
-  const uint32_t sl = static_cast<uint32_t>(key[e] >> shift);
-  if (e == 0 || static_cast<uint32_t>(key[e - 1] >> shift) != sl)
-    atomicMin(&starts[sl], static_cast<unsigned long long>(e));
-}
-
-struct StreamPos {
-  uint64_t start[NSLICE + 1];  // first sorted edge of slice j
-  uint64_t sbase[NSLICE];      // first stream position of slice j
-  uint32_t tbase[NSLICE + 1];  // first global task of slice j
-};
-__device__ __forceinline__ uint32_t slice_of_edge(const StreamPos& P, uint64_t e) {
-  uint32_t j = 0;
-#pragma unroll
-  for (int i = 1; i < NSLICE; ++i) j += e >= P.start[i] ? 1u : 0u;
-  return j;
+  const uint32_t gr = group_of_key(G, key[e]);
+  if (e == 0 || group_of_key(G, key[e - 1]) != gr)
+    atomicMin(&starts[gr], static_cast<unsigned long long>(e));
 }
 
 // col (x position) of every stream edge + the pair-start flags
 __global__ void k_stream_fill(const uint64_t* key, uint64_t n, Layout L, StreamGeo G,
-                              StreamPos P, uint32_t* col, uint32_t* bits32,
-                              unsigned long long* n_pairs) {
+                              const uint64_t* gstart, const uint32_t* gtask, uint32_t* col,
+                              uint32_t* bits32, unsigned long long* n_pairs) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   bool start = false;
   if (e < n) {
     const uint64_t k = key[e];
-    const uint32_t sl = slice_of_edge(P, e);
-    const uint64_t pos = P.sbase[sl] + (e - P.start[sl]);
+    const uint32_t gr = group_of_key(G, k);
+    const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + (e - gstart[gr]);
+    const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
     const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
     const uint32_t qin = static_cast<uint32_t>(k & ((1ull << G.qb) - 1));
-    const uint32_t q = seg ? G.QH + (seg - 1) * G.S + qin : qin;
-    col[pos] = xpos(L, col_of_slice_q(L, G, sl, q));
-    start = e == P.start[sl] || (key[e - 1] >> G.qb) != (k >> G.qb);
+    col[pos] = xpos(L, col_of_slice_q(L, G, sl, q_of_seg(G, seg, qin)));
+    start = e == gstart[gr] || (key[e - 1] >> G.qb) != (k >> G.qb);
     if (start) atomicOr(&bits32[pos / 32], 1u << (pos % 32));
   }
   const uint64_t s = wave_sum_u64(start ? 1u : 0u);
@@ -851,47 +927,43 @@ __global__ void k_stream_fill(const uint64_t* key, uint64_t n, Layout L, StreamG
 }
 
 // pieces of each task (piece starts: the task's first edge and every pair start)
-__global__ void k_task_count(const uint32_t* bits32, StreamPos P, uint32_t ntask, uint32_t* cnt) {
+__global__ void k_task_count(const uint32_t* bits32, uint32_t ntask, uint32_t* cnt) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t > ntask) return;
   if (t == ntask) {
     cnt[t] = 0;
     return;
   }
-  uint32_t j = 0;
-  for (int i = 1; i < NSLICE; ++i) j += t >= P.tbase[i] ? 1u : 0u;
-  const uint64_t w0 = (P.sbase[j] + static_cast<uint64_t>(t - P.tbase[j]) * TASK) / 32;
+  const uint64_t w0 = static_cast<uint64_t>(t) * (TASK / 32);
   uint32_t c = 0;
   for (int i = 0; i < TASK / 32; ++i) c += __popc(bits32[w0 + i] | (i == 0 ? 1u : 0u));
   cnt[t] = c;
 }
 
-// piece index of stream position pos (slice j); also whether pos starts a piece
+// piece index of stream position pos; also whether pos starts a piece
 __device__ __forceinline__ uint32_t piece_of(const uint32_t* bits32, const uint32_t* task_piece,
-                                             const StreamPos& P, uint32_t j, uint64_t pos,
-                                             bool* starts) {
-  const uint64_t rel = pos - P.sbase[j];
-  const uint64_t tl = rel / TASK;
-  const uint64_t w0 = (P.sbase[j] + tl * TASK) / 32, wp = pos / 32;
+                                             uint64_t pos, bool* starts) {
+  const uint64_t t = pos / TASK;
+  const uint64_t w0 = t * (TASK / 32), wp = pos / 32;
   const uint32_t bit = static_cast<uint32_t>(pos % 32);
   uint32_t c = 0;
   for (uint64_t w = w0; w < wp; ++w) c += __popc(bits32[w] & (w == w0 ? ~1u : ~0u));
   const uint32_t last = bits32[wp] & (wp == w0 ? ~1u : ~0u);
   c += __popc(last & (bit == 31 ? ~0u : ((2u << bit) - 1u)));
-  if (starts) *starts = (rel % TASK) == 0 || ((bits32[wp] >> bit) & 1u);
-  return task_piece[P.tbase[j] + tl] + c;
+  if (starts) *starts = (pos % TASK) == 0 || ((bits32[wp] >> bit) & 1u);
+  return task_piece[t] + c;
 }
 
 // row of every piece (from the stream keys)
-__global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, StreamPos P,
-                             const uint32_t* bits32, const uint32_t* task_piece,
-                             uint32_t* piece_row) {
+__global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, const uint64_t* gstart,
+                             const uint32_t* gtask, const uint32_t* bits32,
+                             const uint32_t* task_piece, uint32_t* piece_row) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   if (e >= n) return;
-  const uint32_t sl = slice_of_edge(P, e);
-  const uint64_t pos = P.sbase[sl] + (e - P.start[sl]);
+  const uint32_t gr = group_of_key(G, key[e]);
+  const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + (e - gstart[gr]);
   bool st = false;
-  const uint32_t pc = piece_of(bits32, task_piece, P, sl, pos, &st);
+  const uint32_t pc = piece_of(bits32, task_piece, pos, &st);
   if (st) piece_row[pc] = static_cast<uint32_t>(key[e] >> G.qb) & ((1u << G.rb) - 1u);
 }
 
@@ -929,16 +1001,21 @@ __global__ void k_piece_row_of(const uint32_t* row_pp, const uint32_t* pidx, uin
 }
 __global__ void k_export_keys(const uint32_t* col, const uint32_t* bits32,
                               const uint32_t* task_piece, const uint32_t* piece_row, Layout L,
-                              StreamPos P, uint64_t stream_len, uint64_t* out) {
+                              const uint64_t* gstart, const uint32_t* gtask, uint32_t ngroups,
+                              uint64_t stream_len, uint64_t* out) {
   const uint64_t pos = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   if (pos >= stream_len) return;
-  uint32_t j = 0;
-  for (int i = 1; i < NSLICE; ++i) j += pos >= P.sbase[i] ? 1u : 0u;
-  const uint64_t rel = pos - P.sbase[j];
-  if (rel >= P.start[j + 1] - P.start[j]) return;  // padding
-  const uint32_t pc = piece_of(bits32, task_piece, P, j, pos, nullptr);
+  const uint32_t t = static_cast<uint32_t>(pos / TASK);
+  uint32_t lo = 0, hi = ngroups - 1;  // last group whose first task <= t
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) / 2;
+    if (gtask[mid] <= t) lo = mid; else hi = mid - 1;
+  }
+  const uint64_t rel = pos - static_cast<uint64_t>(gtask[lo]) * TASK;
+  if (rel >= gstart[lo + 1] - gstart[lo]) return;  // padding
+  const uint32_t pc = piece_of(bits32, task_piece, pos, nullptr);
   const uint32_t row = row_of(L, piece_row[pc]);
-  out[P.start[j] + rel] = (static_cast<uint64_t>(row) << 32) | col_of_xpos(L, col[pos]);
+  out[gstart[lo] + rel] = (static_cast<uint64_t>(row) << 32) | col_of_xpos(L, col[pos]);
 }
 __global__ void k_export_split(const uint64_t* key, uint64_t n, uint32_t* col, uint64_t* row_ptr) {
   const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
@@ -1010,6 +1087,7 @@ int env_int(const char* name, int def) {
 void dev_free(DevGraph* g) {
   auto F = [](void* p) { if (p) (void)hipFree(p); };
   F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->row_pp); F(g->pidx);
+  F(g->d_gtask); F(g->d_gstart);
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
   F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->d_bins);
@@ -1056,6 +1134,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.nt = env_int("PR_NT", T.nt);
   T.hot_lds = static_cast<uint32_t>(std::max(0, std::min(20480, env_int("PR_HOTLDS", static_cast<int>(T.hot_lds)))));
   T.dbg = env_int("PR_DBG", 0);
+  T.nlds = std::max(0, std::min(64, env_int("PR_NLDS", T.nlds)));
   T.stream_wg = std::max(1, std::min(2, env_int("PR_STREAM_WG", T.stream_wg)));
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   const uint32_t n = in.n;
@@ -1216,16 +1295,32 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&g->meta, lrows, err));
   if (lrows) hipLaunchKernelGGL(k_local_meta, dim3(grid_for(lrows)), dim3(BLOCK), 0, s, g->perm, g->outdeg, g->dang_w, lrows, g->lA, L, g->meta);
 
+  if (g->X >= (1ull << 28)) {  // gathers address x through a buffer descriptor (2^31 bytes)
+    if (err) *err = "x vector longer than 2^28 entries is not supported";
+    return PR_E_ARG;
+  }
   // ---- stream geometry -----------------------------------------------------------------------
   StreamGeo G{};
   {
     const uint32_t chA = (g->nA + CHUNK - 1) / CHUNK, chC = (g->nC + CHUNK - 1) / CHUNK;
     G.SLq = CHUNK * ((chA + NSLICE - 1) / NSLICE);
     const uint64_t qtot = static_cast<uint64_t>(G.SLq) + CHUNK * ((chC + NSLICE - 1) / NSLICE);
+    // LDS blocks: slice-major x (each slice one contiguous range), byte offsets of x below
+    // 2^31 (buffer loads), blocks inside the class-A part of every slice
+    G.H = HOT_MAX;
+    G.nlds = 0;
+    if (g->sm && g->X < (1ull << 28) && T.hot_lds > 0) {
+      G.H = std::min<uint32_t>(HOT_MAX, T.hot_lds);
+      G.nlds = std::min<uint32_t>(static_cast<uint32_t>(T.nlds), g->SL / G.H);
+    }
+    g->nlds = G.nlds;
+    g->hot_h = G.H;
     G.S = T.seg;
-    G.QH = static_cast<uint32_t>(std::min<uint64_t>(T.qh, std::max<uint64_t>(qtot, 1)));
-    g->nseg = 1u + (qtot > G.QH ? static_cast<uint32_t>((qtot - G.QH + G.S - 1) / G.S) : 0u);
-    G.qb = bits_for(std::max(G.QH, G.S));
+    G.QL = T.qh;
+    const uint64_t ql = static_cast<uint64_t>(G.nlds) * G.H;
+    const uint64_t rest = qtot > ql + G.QL ? qtot - ql - G.QL : 0;
+    g->nseg = G.nlds + 1u + static_cast<uint32_t>((rest + G.S - 1) / G.S);
+    G.qb = bits_for(std::max({G.H, G.QL, G.S}));
     G.rb = bits_for(std::max<uint64_t>(lrows, 2));
     G.sgb = bits_for(std::max<uint64_t>(g->nseg, 2));
   }
@@ -1234,13 +1329,14 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     if (err) *err = "stream keys need more than 64 bits (raise PR_SEG)";
     return PR_E_ARG;
   }
+  const uint32_t NG = NSLICE * (G.nlds + 1);
 
   // ---- local edges: stream keys, stable radix sort -------------------------------------------
   uint64_t* lk_in = uniq == kA ? kB : kA;  // free buffer
-  unsigned long long* d_cnt = nullptr;     // [0] local edges [1] pairs [2..10] slice starts
-  TRY(dmalloc(&d_cnt, 2 + NSLICE, err));
+  unsigned long long* d_cnt = nullptr;     // [0] local edges [1] pairs [2..] group starts
+  TRY(dmalloc(&d_cnt, 2 + NG, err));
   HIPTRY(hipMemsetAsync(d_cnt, 0, 16, s));
-  HIPTRY(hipMemsetAsync(d_cnt + 2, 0xFF, 8 * NSLICE, s));
+  HIPTRY(hipMemsetAsync(d_cnt + 2, 0xFF, 8ull * NG, s));
   if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_for(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, d_cnt, lk_in);
   uint64_t lnnz = nnz;
   if (p > 1) {
@@ -1257,43 +1353,42 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     if (lnnz) HIPTRY(rocprim::radix_sort_keys(tmp.p, tb, db, lnnz, 0, key_bits, s));
     lk = db.current();
   }
-  const int sl_shift = G.sgb + G.rb + G.qb;
-  if (lnnz) hipLaunchKernelGGL(k_slice_starts, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, sl_shift, d_cnt + 2);
-  unsigned long long hst[NSLICE];
-  HIPTRY(hipMemcpyAsync(hst, d_cnt + 2, 8 * NSLICE, hipMemcpyDeviceToHost, s));
+  if (lnnz) hipLaunchKernelGGL(k_group_starts, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, d_cnt + 2);
+  std::vector<unsigned long long> hst(NG);
+  HIPTRY(hipMemcpyAsync(hst.data(), d_cnt + 2, 8ull * NG, hipMemcpyDeviceToHost, s));
   HIPTRY(hipStreamSynchronize(s));
-  StreamPos SP{};
-  SP.start[NSLICE] = lnnz;
-  for (int j = NSLICE - 1; j >= 0; --j) SP.start[j] = std::min<uint64_t>(hst[j], SP.start[j + 1]);
-  uint64_t pos = 0;
-  uint32_t tasks = 0;
-  for (int j = 0; j < NSLICE; ++j) {
-    g->slen[j] = SP.start[j + 1] - SP.start[j];
-    g->sbase[j] = SP.sbase[j] = pos;
-    g->tbase[j] = SP.tbase[j] = tasks;
-    const uint64_t nt = (g->slen[j] + TASK - 1) / TASK;
-    if (tasks + nt > 0xFFFFFFFFull) {
+  g->gstart.assign(NG + 1, lnnz);
+  for (int i = static_cast<int>(NG) - 1; i >= 0; --i) g->gstart[i] = std::min<uint64_t>(hst[i], g->gstart[i + 1]);
+  g->gtask.assign(NG + 1, 0);
+  uint64_t tasks = 0;
+  for (uint32_t i = 0; i < NG; ++i) {
+    g->gtask[i] = static_cast<uint32_t>(tasks);
+    tasks += (g->gstart[i + 1] - g->gstart[i] + TASK - 1) / TASK;
+    if (tasks > 0xFFFFFFF0ull) {
       if (err) *err = "too many stream tasks";
       return PR_E_ARG;
     }
-    tasks += static_cast<uint32_t>(nt);
-    pos += nt * TASK;
   }
-  g->tbase[NSLICE] = SP.tbase[NSLICE] = tasks;
-  g->stream_len = pos;
+  g->gtask[NG] = static_cast<uint32_t>(tasks);
+  g->ntask = static_cast<uint32_t>(tasks);
+  g->stream_len = tasks * TASK;
+  TRY(dmalloc(&g->d_gtask, NG + 1ull, err));
+  TRY(dmalloc(&g->d_gstart, NG + 1ull, err));
+  HIPTRY(hipMemcpyAsync(g->d_gtask, g->gtask.data(), 4ull * (NG + 1), hipMemcpyHostToDevice, s));
+  HIPTRY(hipMemcpyAsync(g->d_gstart, g->gstart.data(), 8ull * (NG + 1), hipMemcpyHostToDevice, s));
 
   // ---- stream arrays: col, pair-start flags, pieces ------------------------------------------
   TRY(dmalloc(&g->col, g->stream_len, err));
   TRY(dmalloc(&g->bits, g->stream_len / EPL + 2, err));
-  HIPTRY(hipMemsetAsync(g->col, 0, 4 * std::max<uint64_t>(g->stream_len, 1), s));
+  HIPTRY(hipMemsetAsync(g->col, 0xFF, 4 * std::max<uint64_t>(g->stream_len, 1), s));  // PAD_COL
   HIPTRY(hipMemsetAsync(g->bits, 0, 2 * (g->stream_len / EPL + 2), s));
   uint32_t* bits32 = reinterpret_cast<uint32_t*>(g->bits);
-  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, SP, g->col, bits32, d_cnt + 1);
+  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, g->d_gstart, g->d_gtask, g->col, bits32, d_cnt + 1);
   TRY(dmalloc(&g->task_piece, tasks + 1ull, err));
   {
     uint32_t* tcnt = nullptr;
     TRY(dmalloc(&tcnt, tasks + 1ull, err));
-    hipLaunchKernelGGL(k_task_count, dim3(grid_for(tasks + 1ull)), dim3(BLOCK), 0, s, bits32, SP, tasks, tcnt);
+    hipLaunchKernelGGL(k_task_count, dim3(grid_for(tasks + 1ull)), dim3(BLOCK), 0, s, bits32, g->ntask, tcnt);
     size_t tb = 0;
     HIPTRY(rocprim::exclusive_scan(nullptr, tb, tcnt, g->task_piece, 0u, tasks + 1ull, rocprim::plus<uint32_t>(), s));
     TRY(tmp.ensure(tb, err));
@@ -1315,7 +1410,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     TRY(dmalloc(&ids, NP, err));
     TRY(dmalloc(&g->pidx, NP, err));
     TRY(dmalloc(&g->row_pp, lrows + 1ull, err));
-    if (lnnz) hipLaunchKernelGGL(k_piece_rows, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, SP, bits32, g->task_piece, prow);
+    if (lnnz) hipLaunchKernelGGL(k_piece_rows, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, g->d_gstart, g->d_gtask, bits32, g->task_piece, prow);
     if (NP) hipLaunchKernelGGL(k_iota, dim3(grid_for(NP)), dim3(BLOCK), 0, s, ids, NP);
     size_t tb = 0;
     HIPTRY(rocprim::radix_sort_pairs(nullptr, tb, prow, prow2, ids, g->pidx, NP, 0, G.rb, s));
@@ -1414,28 +1509,20 @@ double* dev_x_out(DevGraph* g, int t) { return g->xbuf[(t - 1) & 1]; }
 namespace {
 
 void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
-  const bool hot = A.hot_n > 0;
-  const size_t lds = 8ull * (A.hot_n + (STREAM_BLOCK / 64) * STG);
-  // persistent grid: 32 CUs per XCD; one 1024-thread block per CU with the LDS copy of the
-  // hot x prefix (PR_STREAM_WG more without it)
-  const int per_cu = hot ? 1 : std::max(1, g->tune.stream_wg);
+  const size_t lds = 8ull * ((A.nlds ? A.H : 0u) + (STREAM_BLOCK / 64) * STG);
+  // persistent grid: 32 CUs per XCD, one 1024-thread block per CU (the LDS holds one x
+  // block + the staging windows); PR_STREAM_WG blocks per CU without LDS blocks
+  const int per_cu = A.nlds ? 1 : std::max(1, g->tune.stream_wg);
   const dim3 gr(NSLICE * 32 * per_cu), bl(STREAM_BLOCK);
   static bool attr_set = false;  // allow the >64 KB dynamic LDS request
   if (!attr_set) {
-    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<0, true>),
-                          reinterpret_cast<const void*>(&spmv_stream<1, true>),
-                          reinterpret_cast<const void*>(&spmv_stream<0, false>),
-                          reinterpret_cast<const void*>(&spmv_stream<1, false>)})
+    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<0>),
+                          reinterpret_cast<const void*>(&spmv_stream<1>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  if (g->tune.nt) {
-    if (hot) hipLaunchKernelGGL((spmv_stream<1, true>), gr, bl, lds, s, A);
-    else hipLaunchKernelGGL((spmv_stream<1, false>), gr, bl, lds, s, A);
-  } else {
-    if (hot) hipLaunchKernelGGL((spmv_stream<0, true>), gr, bl, lds, s, A);
-    else hipLaunchKernelGGL((spmv_stream<0, false>), gr, bl, lds, s, A);
-  }
+  if (g->tune.nt) hipLaunchKernelGGL((spmv_stream<1>), gr, bl, lds, s, A);
+  else hipLaunchKernelGGL((spmv_stream<0>), gr, bl, lds, s, A);
 }
 
 }  // namespace
@@ -1448,19 +1535,16 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   S.col = g->col;
   S.bits = g->bits;
   S.task_piece = g->task_piece;
+  S.gtask = g->d_gtask;
   S.x_in = x_in;
   S.partial = g->partial;
-  for (int j = 0; j < NSLICE; ++j) {
-    S.sbase[j] = g->sbase[j];
-    S.slen[j] = g->slen[j];
-    S.tbase[j] = g->tbase[j];
+  for (int j = 0; j < NSLICE; ++j)
     S.hot_base[j] = g->sm ? (j % g->p) * g->maxA + (j / g->p) * g->SL : 0u;
-  }
-  // the LDS path addresses x through a buffer descriptor: byte offsets must stay below 2^31
-  S.hot_n = g->sm && g->X < (1ull << 28) ? std::min({g->tune.hot_lds, g->SL, HOT_MAX}) : 0u;
-  S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
+  S.nlds = g->nlds;
+  S.H = g->hot_h;
   S.colmask = g->tune.colmask;
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
+  S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   RowArgs A{};
   A.bins = g->d_bins;
   A.nbins = static_cast<int>(g->bins.size());
@@ -1478,7 +1562,7 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.sm = g->sm ? 1u : 0u;
   A.SL = g->SL;
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
-  if (g->tbase[NSLICE]) launch_stream(g, S, s);
+  if (g->ntask) launch_stream(g, S, s);
   if (g->total_blocks) {
     const dim3 gr(g->total_blocks), bl(BLOCK);
     if (mode == 0) hipLaunchKernelGGL(spmv_rows<0>, gr, bl, 0, s, A);
@@ -1517,16 +1601,6 @@ int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s) {
 
 int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s, std::string* err) {
   const Layout L = layout_of(g);
-  StreamPos SP{};
-  uint64_t acc = 0;
-  for (int j = 0; j < NSLICE; ++j) {
-    SP.start[j] = acc;
-    acc += g->slen[j];
-    SP.sbase[j] = g->sbase[j];
-    SP.tbase[j] = g->tbase[j];
-  }
-  SP.start[NSLICE] = acc;
-  SP.tbase[NSLICE] = g->tbase[NSLICE];
   const uint64_t m = g->lnnz;
   Temp tmp;
   uint32_t* prow = nullptr;
@@ -1542,7 +1616,7 @@ int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s,
   TRY(dmalloc(&rp, g->lrows + 1ull, err)); fr.v.push_back(rp);
   TRY(dmalloc(&c, m, err)); fr.v.push_back(c);
   if (g->lrows) hipLaunchKernelGGL(k_piece_row_of, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->row_pp, g->pidx, g->lrows, prow);
-  if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_for(g->stream_len)), dim3(BLOCK), 0, s, g->col, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, SP, g->stream_len, k0);
+  if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_for(g->stream_len)), dim3(BLOCK), 0, s, g->col, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, g->d_gstart, g->d_gtask, static_cast<uint32_t>(g->gtask.size() - 1), g->stream_len, k0);
   rocprim::double_buffer<uint64_t> db(k0, k1);
   size_t tb = 0;
   HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, m, 0, 64, s));
