@@ -90,11 +90,11 @@ int build_device(pr_ctx* c, const prmi::BuildInput& in) {
   c->last_iters = -1;
   c->host_ranks_valid = false;
   if (c->opts.flags & PR_F_VERBOSE)
-    fprintf(stderr, "[prmi355x] rank %d build %.1f ms: n=%u nnz=%llu rows=%u local_rows=%u local_nnz=%llu segments/slice=%u pairs=%llu pieces=%llu tasks=%u row_bins=%zu row_blocks=%u\n",
+    fprintf(stderr, "[prmi355x] rank %d build %.1f ms: n=%u nnz=%llu rows=%u local_rows=%u local_nnz=%llu segments/slice=%u pairs=%llu pieces=%llu tasks=%u streams=%zu row_blocks=%u\n",
             c->opts.rank, c->dg.ms_build, c->dg.n, (unsigned long long)c->dg.nnz, c->dg.R,
             c->dg.lrows, (unsigned long long)c->dg.lnnz, c->dg.nseg,
             (unsigned long long)c->dg.n_pairs, (unsigned long long)c->dg.n_pieces,
-            c->dg.ntask, c->dg.bins.size(), c->dg.total_blocks);
+            c->dg.ntask, (size_t)c->dg.n_streams, c->dg.nb_rows);
   return PR_OK;
 }
 
@@ -622,7 +622,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   const int nmeas = std::min(done, nk);
   for (int t = 0; t < nmeas; ++t) {
     float k = 0.f;
-    if (g->total_blocks && hipEventElapsedTime(&k, c->kev[2 * t], c->kev[2 * t + 1]) == hipSuccess) kms += k;
+    if (hipEventElapsedTime(&k, c->kev[2 * t], c->kev[2 * t + 1]) == hipSuccess) kms += k;
   }
   s.iterations = done;
   s.ms_total = ms;

@@ -40,15 +40,6 @@ constexpr int CHUNK = 16;          // rows dealt per rank chunk = entries per 12
 constexpr int EPL = 16;            // stream edges per lane per task
 constexpr int TASK = 64 * EPL;     // stream edges per wave task (1024)
 
-// row-kernel kinds 0..6: 2^kind lanes per row; then one workgroup per row
-enum : uint16_t { KIND_BLOCK = 7 };
-
-struct Bin {
-  uint32_t block_begin;  // first tile of this bin in the row launch's grid
-  uint32_t row_begin, row_end;
-  uint16_t kind, cls;    // cls 0 = class A rows, 1 = class B rows
-};
-
 struct IterState {
   double a;          // addthis for the next round (PageRank.java:135-138)
   double resid;      // relative L1 residual of the last round (tracked mode)
@@ -60,10 +51,8 @@ struct IterState {
 };
 
 struct Tuning {
-  int epl = 4;          // row kernel: target pieces per lane
-  uint32_t kb = 1024;   // row kernel: piece count above which one workgroup takes a row
   uint32_t qh = 458752; // PR_QH: L2-hot segment length per slice after the LDS blocks (3.5 MiB)
-  int nlds = 8;         // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
+  int nlds = 12;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
   int nt = 0;           // PR_NT: non-temporal loads for the streamed arrays (slower: 3.8 vs 6 TB/s)
   uint32_t hot_lds = 20480;  // PR_HOTLDS: LDS block length (x entries, capped by the staging room)
@@ -105,8 +94,8 @@ struct DevGraph {
   uint16_t* bits = nullptr;       // [stream_len/16] pair-start flags
   uint32_t* task_piece = nullptr; // [tasks+1] first piece of each task
   double* partial = nullptr;      // [n_pieces] per-piece partial sums
-  uint32_t* row_pp = nullptr;     // [lrows+1] offsets into pidx
-  uint32_t* pidx = nullptr;       // [n_pieces] pieces of each row, stream order
+  uint16_t* roff = nullptr;       // [n_pieces] row of each piece, relative to its row block
+  uint32_t* runs = nullptr;       // [(nb_rows+1) * n_streams] first piece of (row block, stream)
   uint32_t* meta = nullptr;
   uint32_t* perm = nullptr;       // internal -> original
   uint32_t* outdeg = nullptr;     // by original id
@@ -120,10 +109,8 @@ struct DevGraph {
   uint64_t* rec_local = nullptr;  // [REC_WORDS]
   uint64_t* rec_all = nullptr;    // [p][REC_WORDS]
   IterState* state = nullptr;
-  // row launch schedule
-  std::vector<Bin> bins;
-  Bin* d_bins = nullptr;
-  uint32_t total_blocks = 0;
+  // row launch: blocks of 1024 rows (class A, then class B), streams = slices x segments
+  uint32_t nb_rows = 0, nb_rows_a = 0, n_streams = 0;
   Tuning tune;
 };
 

@@ -157,14 +157,21 @@ __device__ double sa_to_double_dev(const uint64_t* limb) {
 // =======================================================================================
 // the round: slice streams (per-piece partial sums) + fused row launch (combine + epilogue)
 // =======================================================================================
-// Row launch: a row's value c = fixed-order sum of its pieces' partials, then PageRank.java's
-// damping / contribution epilogue.
+// Row launch: rows are cut into blocks of RB rows (class-A blocks, then class-B blocks).  For
+// every block and every stream k = (slice, segment), the block's pieces of stream k are one
+// contiguous run of the partial array (pieces are in stream order, rows ascending inside a
+// stream): T[block][k] = first piece of the run, T[block + 1][k] = one past it.  Each wave
+// adds a fixed quarter of the block's runs (concatenated in stream order) into its own LDS
+// accumulator; c[row] = (acc0 + acc1) + (acc2 + acc3).  Then PageRank.java's damping /
+// contribution epilogue.
+constexpr int RB = 1024;           // rows per row-launch block
+constexpr int MAX_NS = 512;        // streams (slices x segments) the row launch supports
+constexpr int EPR = 8;             // pieces per lane per step (16 measured slower)
 struct RowArgs {
-  const Bin* bins;
-  int nbins;
-  const uint32_t* row_pp;  // [lrows+1] offsets into pidx
-  const uint32_t* pidx;    // pieces of each row (stream order)
+  const uint32_t* T;       // [(NB + 1) * NS] run starts
   const double* partial;   // per-piece partial sums of this round
+  const uint16_t* roff;    // per-piece row offset inside its block
+  uint32_t NS, nbA, lA, lrows;
   const uint32_t* meta;
   double* x_out;           // this rank's slot of the next x
   const double* r_old;     // tracked mode: previous ranks (nullptr = r^0 == 1)
@@ -181,59 +188,12 @@ __device__ __forceinline__ uint32_t xslot_of(const RowArgs& A, uint32_t l) {
   return (sl / A.p) * A.SL + (c / NSLICE) * CHUNK + (l % CHUNK);
 }
 
-__device__ __forceinline__ int find_bin(const Bin* bins, int nbins, uint32_t t) {
-  int lo = 0, hi = nbins - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (bins[mid].block_begin <= t) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
-// Streamed (read-once) operands: non-temporal loads keep them from evicting the hot part
-// of x from the XCD's L2 (NT = 1).
+// Streamed (read-once) operands: non-temporal loads (NT = 1) were measured slower than
+// regular loads for streams (3.8 vs 6.0 TB/s, scripts/probes/stream_probe.hip).
 template <int NT, class T>
 __device__ __forceinline__ T ld_stream(const T* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
   else return *p;
-}
-
-struct GatherX {
-  const double* __restrict__ x;
-  __device__ __forceinline__ double operator()(uint32_t q) const { return x[q]; }
-};
-
-// Partial sum of x[col[e]] over e = beg + lane, beg + lane + S, ... < end, with four
-// independent gathers in flight per lane.  Fixed order: depends on (end-beg, S) only.
-template <int S, int NT, class Gx>
-__device__ __forceinline__ double strided_sum(const uint32_t* __restrict__ col, const Gx& gx,
-                                              uint64_t beg, uint64_t end, int lane) {
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  for (uint64_t e = beg + lane; e < end; e += 4ull * S) {
-    const uint64_t e1 = e + S, e2 = e + 2ull * S, e3 = e + 3ull * S;
-    const uint32_t c0 = ld_stream<NT>(col + e);
-    const uint32_t c1 = e1 < end ? ld_stream<NT>(col + e1) : 0u;
-    const uint32_t c2 = e2 < end ? ld_stream<NT>(col + e2) : 0u;
-    const uint32_t c3 = e3 < end ? ld_stream<NT>(col + e3) : 0u;
-    const double v0 = gx(c0);
-    const double v1 = e1 < end ? gx(c1) : 0.0;
-    const double v2 = e2 < end ? gx(c2) : 0.0;
-    const double v3 = e3 < end ? gx(c3) : 0.0;
-    s0 += v0;
-    s1 += v1;
-    s2 += v2;
-    s3 += v3;
-  }
-  return (s0 + s1) + (s2 + s3);
-}
-
-// Workgroup-wide sum (fixed tree), valid in thread 0.
-__device__ __forceinline__ double block_sum(double s, double* red) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // Epilogue for one row per group leader, then the block's exact partials (dangling mass +
@@ -286,49 +246,92 @@ __device__ __forceinline__ void row_epilogue(const RowArgs& A, double a, uint32_
   }
 }
 
-// G lanes per row (G <= 64): a workgroup takes 256/G consecutive rows of one bin; the row's
-// pieces are summed with strided_sum (shape fixed by the piece count and G).
-template <int G, int MODE>
-__device__ __forceinline__ void group_tile(const RowArgs& A, double a, const Bin& b,
-                                           uint32_t blk, uint64_t (*lds)[REC_WORDS]) {
-  constexpr uint32_t RPB = BLOCK / G;
-  const uint32_t row = b.row_begin + blk * RPB + threadIdx.x / G;
-  const int gl = threadIdx.x % G;
-  const bool active = row < b.row_end;
-  double s = 0.0;
-  if (active)
-    s = strided_sum<G, 0>(A.pidx, GatherX{A.partial}, A.row_pp[row], A.row_pp[row + 1], gl);
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-  row_epilogue<MODE>(A, a, b.cls, row, s, active && gl == 0, lds);
-}
-
 // The row launch (PageRank.java:139-145 reduceByKey(Sum) + mapValues, and the inputs of
 // :113 and :125-134 for the next round).
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
+  __shared__ double acc[4][RB];
+  __shared__ uint32_t pre[MAX_NS + 1], st[MAX_NS];
+  __shared__ uint32_t wtot[4];
   __shared__ uint64_t lds[4][REC_WORDS];
-  __shared__ double red[4];
   const uint32_t b = blockIdx.x;
-  const Bin bin = A.bins[find_bin(A.bins, A.nbins, b)];
-  const uint32_t blk = b - bin.block_begin;
-  const double a = A.st->a;
-  switch (bin.kind) {
-    case 0: group_tile<1, MODE>(A, a, bin, blk, lds); break;
-    case 1: group_tile<2, MODE>(A, a, bin, blk, lds); break;
-    case 2: group_tile<4, MODE>(A, a, bin, blk, lds); break;
-    case 3: group_tile<8, MODE>(A, a, bin, blk, lds); break;
-    case 4: group_tile<16, MODE>(A, a, bin, blk, lds); break;
-    case 5: group_tile<32, MODE>(A, a, bin, blk, lds); break;
-    case 6: group_tile<64, MODE>(A, a, bin, blk, lds); break;
-    default: {  // KIND_BLOCK: one workgroup per row
-      const uint32_t row = bin.row_begin + blk;
-      double s = strided_sum<BLOCK, 0>(A.pidx, GatherX{A.partial}, A.row_pp[row],
-                                       A.row_pp[row + 1], threadIdx.x);
-      s = block_sum(s, red);
-      row_epilogue<MODE>(A, a, bin.cls, row, s, threadIdx.x == 0, lds);
-      break;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < 4 * RB; i += BLOCK) (&acc[0][0])[i] = 0.0;
+  // run lengths of the block's streams -> exclusive prefix pre[] (two streams per thread)
+  const uint32_t NS = A.NS;
+  const uint32_t* T0 = A.T + static_cast<uint64_t>(b) * NS;
+  const uint32_t k0 = 2 * tid, k1 = 2 * tid + 1;
+  uint32_t len0 = 0, len1 = 0;
+  if (k0 < NS) {
+    st[k0] = T0[k0];
+    len0 = T0[NS + k0] - T0[k0];
+  }
+  if (k1 < NS) {
+    st[k1] = T0[k1];
+    len1 = T0[NS + k1] - T0[k1];
+  }
+  uint32_t inc = len0 + len1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) wtot[wv] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int i = 0; i < wv; ++i) base += wtot[i];
+  const uint32_t ex = base + inc - len0 - len1;
+  if (k0 < NS) pre[k0] = ex;
+  if (k1 < NS) pre[k1] = ex + len0;
+  if (tid == 0) pre[NS] = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+  __syncthreads();
+  // this wave's quarter of the concatenated runs, EPR consecutive pieces per lane per step
+  const uint32_t total = pre[NS];
+  const uint32_t lo = static_cast<uint32_t>(static_cast<uint64_t>(total) * wv / 4);
+  const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (wv + 1) / 4);
+  double* aw = acc[wv];
+  uint32_t kw = 0;  // wave-uniform lower bound of the stream search
+  for (uint32_t pos = lo; pos < hi; pos += 64 * EPR) {
+    const uint32_t i0 = pos + lane * EPR;
+    // stream of i0: last k with pre[k] <= i0 (empty streams share pre with the next one)
+    uint32_t k = kw, kh = NS - 1;
+    while (k < kh) {
+      const uint32_t mid = (k + kh + 1) >> 1;
+      if (pre[mid] <= i0) k = mid; else kh = mid - 1;
     }
+    uint32_t pc[EPR];
+#pragma unroll
+    for (int u = 0; u < EPR; ++u) {
+      const uint32_t i = i0 + u;
+      while (k + 1 < NS && pre[k + 1] <= i) ++k;
+      pc[u] = i < hi ? st[k] + (i - pre[k]) : 0u;  // never address past the pieces
+    }
+    double val[EPR];
+    uint32_t r[EPR];
+#pragma unroll
+    for (int u = 0; u < EPR; ++u) {
+      const bool ok = i0 + u < hi;
+      val[u] = A.partial[pc[u]];
+      r[u] = A.roff[pc[u]];
+      if (!ok) val[u] = 0.0;
+    }
+    // LDS adds in lane order inside each instruction: a fixed order for a fixed layout
+#pragma unroll
+    for (int u = 0; u < EPR; ++u)
+      if (i0 + u < hi) atomicAdd(&aw[r[u]], val[u]);
+    kw = __builtin_amdgcn_readfirstlane(k);  // lane 0's stream after this step (monotone)
+  }
+  __syncthreads();
+  // epilogue over the block's rows (uniform trip count: row_epilogue synchronises)
+  const bool clsB = b >= A.nbA;
+  const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * RB : b * RB;
+  const uint32_t rb1 = min(rb0 + RB, clsB ? A.lrows : A.lA);
+  const double a = A.st->a;
+  for (int l = tid; l < RB; l += BLOCK) {
+    const uint32_t row = rb0 + l;
+    const bool active = row < rb1;
+    const double c = (acc[0][l] + acc[1][l]) + (acc[2][l] + acc[3][l]);
+    row_epilogue<MODE>(A, a, clsB ? 1u : 0u, row, c, active, lds);
   }
 }
 
@@ -799,6 +802,7 @@ __global__ void k_x_init(const uint32_t* perm, const uint32_t* outdeg, uint32_t 
 // ranges of S entries.  Stream groups per slice: one per LDS block + one for everything
 // after it; every group starts on a task boundary (padding: col = PAD, gathers read 0).
 constexpr uint32_t PAD_COL = 0xFFFFFFFFu;
+static_assert(PAD_COL == 0xFFFFFFFFu, "the build pads col with memset(0xFF)");
 struct StreamGeo {
   uint32_t SLq;       // q-space length of the class-A part of one slice
   uint32_t nlds, H;   // LDS blocks per slice and their length
@@ -954,17 +958,47 @@ __device__ __forceinline__ uint32_t piece_of(const uint32_t* bits32, const uint3
   return task_piece[t] + c;
 }
 
-// row of every piece (from the stream keys)
-__global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, const uint64_t* gstart,
-                             const uint32_t* gtask, const uint32_t* bits32,
-                             const uint32_t* task_piece, uint32_t* piece_row) {
+// row and stream (slice * nseg + segment) of every piece (from the stream keys)
+__global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, uint32_t nseg,
+                             const uint64_t* gstart, const uint32_t* gtask, const uint32_t* bits32,
+                             const uint32_t* task_piece, uint32_t* piece_row,
+                             uint32_t* piece_stream) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   if (e >= n) return;
-  const uint32_t gr = group_of_key(G, key[e]);
+  const uint64_t k = key[e];
+  const uint32_t gr = group_of_key(G, k);
   const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + (e - gstart[gr]);
   bool st = false;
   const uint32_t pc = piece_of(bits32, task_piece, pos, &st);
-  if (st) piece_row[pc] = static_cast<uint32_t>(key[e] >> G.qb) & ((1u << G.rb) - 1u);
+  if (st) {
+    piece_row[pc] = static_cast<uint32_t>(k >> G.qb) & ((1u << G.rb) - 1u);
+    const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
+    const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
+    piece_stream[pc] = sl * nseg + seg;
+  }
+}
+
+// row blocks of the row launch: class-A rows in blocks of RB, then class-B rows
+struct RowBlocks {
+  uint32_t lA, nbA, NB, NS;
+};
+__device__ __forceinline__ uint32_t block_of_row(const RowBlocks& B, uint32_t l) {
+  return l < B.lA ? l / RB : B.nbA + (l - B.lA) / RB;
+}
+__device__ __forceinline__ uint32_t block_row0(const RowBlocks& B, uint32_t b) {
+  return b < B.nbA ? b * RB : B.lA + (b - B.nbA) * RB;
+}
+
+// per-piece row offset in its block + run starts T[block][stream] (sentinel where empty)
+__global__ void k_runs(const uint32_t* prow, const uint32_t* pstream, uint64_t np, RowBlocks B,
+                       uint16_t* roff, uint32_t* T, uint32_t* sstart) {
+  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (i >= np) return;
+  const uint32_t l = prow[i], k = pstream[i], b = block_of_row(B, l);
+  roff[i] = static_cast<uint16_t>(l - block_row0(B, b));
+  const bool first = i == 0 || pstream[i - 1] != k || block_of_row(B, prow[i - 1]) != b;
+  if (first) T[static_cast<uint64_t>(b) * B.NS + k] = static_cast<uint32_t>(i);
+  if (i == 0 || pstream[i - 1] != k) sstart[k] = static_cast<uint32_t>(i);
 }
 
 __global__ void k_fill_f64(double* a, uint64_t n, double v) {
@@ -977,13 +1011,6 @@ __global__ void k_iota(uint32_t* a, uint64_t n) {
   if (i < n) a[i] = static_cast<uint32_t>(i);
 }
 
-// row_pp[r] = first position of row r in the row-sorted piece list (every row has one)
-__global__ void k_row_starts(const uint32_t* rows_sorted, uint64_t n, uint32_t* row_pp) {
-  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (i >= n) return;
-  if (i == 0 || rows_sorted[i - 1] != rows_sorted[i]) row_pp[rows_sorted[i]] = static_cast<uint32_t>(i);
-}
-
 __global__ void k_local_meta(const uint32_t* perm, const uint32_t* outdeg, const uint32_t* dang_w,
                              uint32_t lrows, uint32_t lA, Layout L, uint32_t* meta) {
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
@@ -993,11 +1020,13 @@ __global__ void k_local_meta(const uint32_t* perm, const uint32_t* outdeg, const
 }
 
 // export: (internal row << 32 | internal source) of every stream edge
-__global__ void k_piece_row_of(const uint32_t* row_pp, const uint32_t* pidx, uint32_t lrows,
-                               uint32_t* piece_row) {
-  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= lrows) return;
-  for (uint32_t k = row_pp[l]; k < row_pp[l + 1]; ++k) piece_row[pidx[k]] = l;
+__global__ void k_piece_row_runs(const uint32_t* T, const uint16_t* roff, RowBlocks B,
+                                 uint32_t* piece_row) {
+  const uint64_t t = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (t >= static_cast<uint64_t>(B.NB) * B.NS) return;
+  const uint32_t b = static_cast<uint32_t>(t / B.NS);
+  const uint32_t r0 = block_row0(B, b);
+  for (uint32_t i = T[t]; i < T[t + B.NS]; ++i) piece_row[i] = r0 + roff[i];
 }
 __global__ void k_export_keys(const uint32_t* col, const uint32_t* bits32,
                               const uint32_t* task_piece, const uint32_t* piece_row, Layout L,
@@ -1086,11 +1115,11 @@ int env_int(const char* name, int def) {
 
 void dev_free(DevGraph* g) {
   auto F = [](void* p) { if (p) (void)hipFree(p); };
-  F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->row_pp); F(g->pidx);
+  F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->roff); F(g->runs);
   F(g->d_gtask); F(g->d_gstart);
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
-  F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->d_bins);
+  F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state);
   const int p = g->p, rank = g->rank;
   *g = DevGraph();
   g->p = p;
@@ -1112,13 +1141,6 @@ uint32_t owned_rows(uint32_t cnt, uint32_t p, uint32_t j) {
   return r;
 }
 
-uint16_t kind_for(uint64_t len, const Tuning& T) {
-  if (len > T.kb) return KIND_BLOCK;
-  const uint64_t want = (len + T.epl - 1) / T.epl;
-  uint16_t kd = 0;
-  while ((1ull << kd) < want && kd < 6) ++kd;
-  return kd;
-}
 
 }  // namespace
 
@@ -1127,8 +1149,6 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   const int p = g->p, rank = g->rank;
   dev_free(g);
   Tuning& T = g->tune;
-  T.epl = std::max(1, env_int("PR_EPL", T.epl));
-  T.kb = static_cast<uint32_t>(std::max(64, env_int("PR_KB", static_cast<int>(T.kb))));
   T.qh = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_QH", static_cast<int>(T.qh))));
   T.seg = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_SEG", static_cast<int>(T.seg))));
   T.nt = env_int("PR_NT", T.nt);
@@ -1403,27 +1423,55 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     g->n_pairs = npairs;
   }
   const uint64_t NP = g->n_pieces;
+  // ---- row launch: row blocks, per-piece row offsets, run table ------------------------------
+  RowBlocks RBk{};
+  RBk.lA = g->lA;
+  RBk.nbA = (g->lA + RB - 1) / RB;
+  RBk.NB = RBk.nbA + (lrows - g->lA + RB - 1) / RB;
+  RBk.NS = NSLICE * g->nseg;
+  if (RBk.NS > static_cast<uint32_t>(MAX_NS)) {
+    if (err) *err = "too many stream segments for the row launch (raise PR_SEG)";
+    return PR_E_ARG;
+  }
+  g->nb_rows = RBk.NB;
+  g->nb_rows_a = RBk.nbA;
+  g->n_streams = RBk.NS;
   {
-    uint32_t *prow = nullptr, *prow2 = nullptr, *ids = nullptr;
+    uint32_t *prow = nullptr, *pstream = nullptr, *sst = nullptr;
     TRY(dmalloc(&prow, NP, err));
-    TRY(dmalloc(&prow2, NP, err));
-    TRY(dmalloc(&ids, NP, err));
-    TRY(dmalloc(&g->pidx, NP, err));
-    TRY(dmalloc(&g->row_pp, lrows + 1ull, err));
-    if (lnnz) hipLaunchKernelGGL(k_piece_rows, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, g->d_gstart, g->d_gtask, bits32, g->task_piece, prow);
-    if (NP) hipLaunchKernelGGL(k_iota, dim3(grid_for(NP)), dim3(BLOCK), 0, s, ids, NP);
-    size_t tb = 0;
-    HIPTRY(rocprim::radix_sort_pairs(nullptr, tb, prow, prow2, ids, g->pidx, NP, 0, G.rb, s));
-    TRY(tmp.ensure(tb, err));
-    if (NP) HIPTRY(rocprim::radix_sort_pairs(tmp.p, tb, prow, prow2, ids, g->pidx, NP, 0, G.rb, s));
-    HIPTRY(hipMemsetAsync(g->row_pp, 0xFF, 4ull * (lrows + 1), s));
-    if (NP) hipLaunchKernelGGL(k_row_starts, dim3(grid_for(NP)), dim3(BLOCK), 0, s, prow2, NP, g->row_pp);
-    const uint32_t np32 = static_cast<uint32_t>(NP);
-    HIPTRY(hipMemcpyAsync(g->row_pp + lrows, &np32, 4, hipMemcpyHostToDevice, s));
+    TRY(dmalloc(&pstream, NP, err));
+    TRY(dmalloc(&sst, RBk.NS, err));
+    TRY(dmalloc(&g->roff, NP, err));
+    const uint64_t tn = (RBk.NB + 1ull) * RBk.NS;
+    TRY(dmalloc(&g->runs, tn, err));
+    HIPTRY(hipMemsetAsync(g->runs, 0xFF, 4 * tn, s));
+    HIPTRY(hipMemsetAsync(sst, 0xFF, 4ull * RBk.NS, s));
+    if (lnnz) hipLaunchKernelGGL(k_piece_rows, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, g->nseg, g->d_gstart, g->d_gtask, bits32, g->task_piece, prow, pstream);
+    if (NP) hipLaunchKernelGGL(k_runs, dim3(grid_for(NP)), dim3(BLOCK), 0, s, prow, pstream, NP, RBk, g->roff, g->runs, sst);
+    // fill the empty runs: T[NB][k] = end of stream k, T[b][k] = T[b+1][k] where empty
+    std::vector<uint32_t> hT(tn), hs(RBk.NS);
+    HIPTRY(hipMemcpyAsync(hT.data(), g->runs, 4 * tn, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(hs.data(), sst, 4ull * RBk.NS, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    const uint32_t NSs = RBk.NS;
+    std::vector<uint32_t> send(NSs);
+    uint32_t nxt = static_cast<uint32_t>(NP);
+    for (int k = static_cast<int>(NSs) - 1; k >= 0; --k) {
+      send[k] = nxt;
+      if (hs[k] != 0xFFFFFFFFu) nxt = hs[k];
+    }
+    for (uint32_t k = 0; k < NSs; ++k) {
+      hT[static_cast<uint64_t>(RBk.NB) * NSs + k] = send[k];
+      for (int bb = static_cast<int>(RBk.NB) - 1; bb >= 0; --bb) {
+        uint32_t& v = hT[static_cast<uint64_t>(bb) * NSs + k];
+        if (v == 0xFFFFFFFFu) v = hT[static_cast<uint64_t>(bb + 1) * NSs + k];
+      }
+    }
+    HIPTRY(hipMemcpyAsync(g->runs, hT.data(), 4 * tn, hipMemcpyHostToDevice, s));
     HIPTRY(hipStreamSynchronize(s));
     (void)hipFree(prow);
-    (void)hipFree(prow2);
-    (void)hipFree(ids);
+    (void)hipFree(pstream);
+    (void)hipFree(sst);
   }
   HIPTRY(hipGetLastError());
   (void)hipFree(d_cnt);
@@ -1434,47 +1482,6 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&g->partial, NP, err));
   // PR_DBG experiments may skip the partial stores: keep every rank defined
   if (T.dbg && NP) hipLaunchKernelGGL(k_fill_f64, dim3(grid_for(NP)), dim3(BLOCK), 0, s, g->partial, NP, 1.0);
-
-  // ---- row launch schedule: bins of equal lanes-per-row over the row-sorted piece counts ----
-  {
-    std::vector<uint32_t> hpp(lrows + 1ull);
-    HIPTRY(hipMemcpyAsync(hpp.data(), g->row_pp, 4ull * (lrows + 1), hipMemcpyDeviceToHost, s));
-    HIPTRY(hipStreamSynchronize(s));
-    for (uint32_t l = 0; l < lrows; ++l)
-      if (hpp[l] >= hpp[l + 1]) {
-        if (err) *err = "internal: a local row without pieces";
-        return PR_E_HIP;
-      }
-    uint32_t blocks = 0;
-    for (int cls = 0; cls < 2; ++cls) {
-      const uint32_t r0 = cls ? g->lA : 0, r1 = cls ? lrows : g->lA;
-      if (r1 <= r0) continue;
-      // lanes per row: non-increasing along the (in-degree sorted) rows -> few bins
-      std::vector<uint16_t> kd(r1 - r0);
-      uint16_t run = 0;
-      for (uint32_t l = r1; l-- > r0;) {
-        run = std::max(run, kind_for(hpp[l + 1] - hpp[l], T));
-        kd[l - r0] = run;
-      }
-      uint32_t i = r0;
-      while (i < r1) {
-        uint32_t e = i + 1;
-        while (e < r1 && kd[e - r0] == kd[i - r0]) ++e;
-        Bin b{};
-        b.block_begin = blocks;
-        b.row_begin = i;
-        b.row_end = e;
-        b.kind = kd[i - r0];
-        b.cls = static_cast<uint16_t>(cls);
-        blocks += b.kind == KIND_BLOCK ? e - i : (e - i + (BLOCK >> b.kind) - 1) / (BLOCK >> b.kind);
-        g->bins.push_back(b);
-        i = e;
-      }
-    }
-    g->total_blocks = blocks;
-    TRY(dmalloc(&g->d_bins, g->bins.size(), err));
-    if (!g->bins.empty()) HIPTRY(hipMemcpyAsync(g->d_bins, g->bins.data(), g->bins.size() * sizeof(Bin), hipMemcpyHostToDevice, s));
-  }
 
   // ---- iteration buffers ----------------------------------------------------------------
   TRY(dmalloc(&g->r_loc[0], lrows, err));
@@ -1546,11 +1553,13 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   RowArgs A{};
-  A.bins = g->d_bins;
-  A.nbins = static_cast<int>(g->bins.size());
-  A.row_pp = g->row_pp;
-  A.pidx = g->pidx;
+  A.T = g->runs;
   A.partial = g->partial;
+  A.roff = g->roff;
+  A.NS = g->n_streams;
+  A.nbA = g->nb_rows_a;
+  A.lA = g->lA;
+  A.lrows = g->lrows;
   A.meta = g->meta;
   A.x_out = dev_x_out(g, t) + static_cast<uint64_t>(g->rank) * g->maxA;
   A.r_old = t == 1 ? nullptr : g->r_loc[(t - 1) & 1];
@@ -1563,8 +1572,8 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.SL = g->SL;
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
   if (g->ntask) launch_stream(g, S, s);
-  if (g->total_blocks) {
-    const dim3 gr(g->total_blocks), bl(BLOCK);
+  if (g->nb_rows) {
+    const dim3 gr(g->nb_rows), bl(BLOCK);
     if (mode == 0) hipLaunchKernelGGL(spmv_rows<0>, gr, bl, 0, s, A);
     else if (mode == 1) hipLaunchKernelGGL(spmv_rows<1>, gr, bl, 0, s, A);
     else hipLaunchKernelGGL(spmv_rows<2>, gr, bl, 0, s, A);
@@ -1615,7 +1624,8 @@ int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s,
   TRY(dmalloc(&k1, m, err)); fr.v.push_back(k1);
   TRY(dmalloc(&rp, g->lrows + 1ull, err)); fr.v.push_back(rp);
   TRY(dmalloc(&c, m, err)); fr.v.push_back(c);
-  if (g->lrows) hipLaunchKernelGGL(k_piece_row_of, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->row_pp, g->pidx, g->lrows, prow);
+  const RowBlocks RBk{g->lA, g->nb_rows_a, g->nb_rows, g->n_streams};
+  if (g->nb_rows) hipLaunchKernelGGL(k_piece_row_runs, dim3(grid_for(static_cast<uint64_t>(g->nb_rows) * g->n_streams)), dim3(BLOCK), 0, s, g->runs, g->roff, RBk, prow);
   if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_for(g->stream_len)), dim3(BLOCK), 0, s, g->col, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, g->d_gstart, g->d_gtask, static_cast<uint32_t>(g->gtask.size() - 1), g->stream_len, k0);
   rocprim::double_buffer<uint64_t> db(k0, k1);
   size_t tb = 0;
