@@ -82,15 +82,19 @@ struct DevGraph {
   // [gstart[gr], gstart[gr+1]) (a group's tail task is padded with PAD_COL edges)
   std::vector<uint32_t> gtask;
   std::vector<uint64_t> gstart;
+  std::vector<uint64_t> gbase;    // first edge of each group in col16 (LDS groups) / col (L2)
   uint32_t* d_gtask = nullptr;
   uint64_t* d_gstart = nullptr;
+  uint64_t* d_gbase = nullptr;
+  uint64_t n_col16 = 0, n_col32 = 0;
   uint32_t ntask = 0;
   uint32_t nlds = 0, hot_h = 0;   // LDS blocks per slice and their length (x entries)
   uint32_t nseg = 0;              // segments per slice (LDS blocks + L2-hot + cold)
   uint64_t n_pieces = 0, n_pairs = 0;
   uint64_t stream_len = 0;        // padded length of col (multiple of TASK)
   // device arrays
-  uint32_t* col = nullptr;        // [stream_len] x position of each stream edge
+  uint32_t* col = nullptr;        // [n_col32] L2-group edges: x position of the source
+  uint16_t* col16 = nullptr;      // [n_col16] LDS-group edges: source offset inside the block
   uint16_t* bits = nullptr;       // [stream_len/16] pair-start flags
   uint32_t* task_piece = nullptr; // [tasks+1] first piece of each task
   double* partial = nullptr;      // [n_pieces] per-piece partial sums

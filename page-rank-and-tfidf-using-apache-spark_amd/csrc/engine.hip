@@ -344,7 +344,9 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
 // a lane; pieces that cross lanes are joined by a segmented scan over the wave.  Every
 // summation order is fixed by the stream layout (deterministic).
 struct StreamArgs {
-  const uint32_t* col;
+  const uint32_t* col;       // L2-group edges: x position (u32)
+  const uint16_t* col16;     // LDS-group edges: offset inside the LDS block (u16; H = zero slot)
+  const uint64_t* gbase;     // [groups] first edge of each group in col / col16
   const uint16_t* bits;
   const uint32_t* task_piece;
   const uint32_t* gtask;     // [8 * (nlds + 1) + 1] first task of each stream group
@@ -359,7 +361,8 @@ struct StreamArgs {
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 128;           // per-wave LDS staging window for piece stores (doubles)
-constexpr uint32_t HOT_MAX = 20480 - (STREAM_BLOCK / 64) * STG;  // LDS left for the x block
+// LDS left for the x block: H entries + a zero slot (index H, the 16-bit padding column)
+constexpr uint32_t HOT_MAX = 20480 - (STREAM_BLOCK / 64) * STG - 8;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -419,57 +422,75 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(x), static_cast<short>(0),
                                         static_cast<int>(A.x_bytes), 0x00020000);
   const uint32_t* __restrict__ col = A.col;
+  const uint16_t* __restrict__ col16 = A.col16;
   const uint16_t* __restrict__ bits = A.bits;
   const uint32_t* __restrict__ tpa = A.task_piece;
   double* __restrict__ part = A.partial;
   const uint32_t cm = A.colmask;
   const uint32_t ngs = A.nlds + 1;
-  double* stg = hot + A.H * (A.nlds ? 1u : 0u) + (threadIdx.x >> 6) * STG;
-  // software pipeline: the next task's stream words are in flight while this task gathers
+  double* stg = hot + (A.nlds ? A.H + 8u : 0u) + (threadIdx.x >> 6) * STG;
+  // software pipeline: the next task's stream words are in flight while this task gathers.
+  // An LDS-group task is 16 x u16 per lane (two 16-byte loads), an L2 task 16 x u32 (four).
   u32x4 cn[4];
   uint32_t bnx = 0, tpn = 0;
-  auto fetch = [&](uint32_t tt) {
-    const uint64_t o = static_cast<uint64_t>(tt) * TASK + lane * EPL;
-    // groups are padded to whole tasks: these loads never leave the stream buffer
-    const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
+  const uint32_t l2g = j * ngs + A.nlds;
+  const uint32_t l2b = A.gtask[l2g], l2e = A.gtask[l2g + 1];
+  const uint64_t l2base = A.gbase[l2g];
+  auto fetch = [&](uint32_t tt, bool lds_task, uint32_t gtb, uint64_t gbs) {
+    const uint64_t o = gbs + static_cast<uint64_t>(tt - gtb) * TASK + lane * EPL;
+    // groups are padded to whole tasks: these loads never leave the stream buffers
+    if (lds_task) {
+      const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
+      cn[0] = cp[0];
+      cn[1] = cp[1];
+    } else {
+      const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) cn[q] = ld_stream<NT>(cp + q);
-    bnx = ld_stream<NT>(bits + o / EPL);
+      for (int q = 0; q < 4; ++q) cn[q] = cp[q];
+    }
+    const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
+    bnx = bits[so / EPL];
     tpn = tpa[tt];
   };
-  // the slice's groups in order: LDS blocks 0..nlds-1 (each with its own LDS fill), then
-  // the L2 part (no LDS block)
   // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
   // with 1/nlds of the L2 part's tasks (LDS-bound and L2-bound work side by side); with no
   // LDS blocks the single phase is the whole stream.
-  const uint32_t l2b = A.gtask[j * ngs + A.nlds], l2e = A.gtask[j * ngs + A.nlds + 1];
   const uint32_t nph = A.nlds ? A.nlds : 1u;
   for (uint32_t gi = 0; gi < nph; ++gi) {
     uint32_t tb = l2b, te = l2b, rb = l2b, re = l2e;  // LDS-block tasks, L2 share
-    uint32_t hb = 0, Hs = 0;
+    uint64_t lbase = 0;
     if (A.nlds) {
       tb = A.gtask[j * ngs + gi];
       te = A.gtask[j * ngs + gi + 1];
+      lbase = A.gbase[j * ngs + gi];
       rb = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * gi) / A.nlds);
       re = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * (gi + 1)) / A.nlds);
-      hb = A.hot_base[j] + gi * A.H;
-      Hs = A.H;
+      const uint32_t hb = A.hot_base[j] + gi * A.H;
       __syncthreads();  // every wave is done with the previous block
-      if (te > tb)
-        for (uint32_t i = threadIdx.x; i < Hs; i += blockDim.x) hot[i] = x[hb + i];
+      if (te > tb) {
+        for (uint32_t i = threadIdx.x; i < A.H; i += blockDim.x) hot[i] = x[hb + i];
+        if (threadIdx.x == 0) hot[A.H] = 0.0;  // the padding column
+      }
       __syncthreads();
     }
     const uint32_t nL = te - tb, nR = re - rb, nm = min(nL, nR);
     // virtual index u -> task: alternate LDS / L2 tasks while both last, then the rest
+    auto is_lds = [&](uint32_t u) -> bool {
+      if (u < 2 * nm) return (u & 1u) == 0u;
+      return nL > nR;
+    };
     auto task_of = [&](uint32_t u) -> uint32_t {
       if (u < 2 * nm) return (u & 1u) ? rb + (u >> 1) : tb + (u >> 1);
       return nL > nR ? tb + (u - nm) : rb + (u - nm);
     };
+    auto fetch_u = [&](uint32_t u) {
+      const bool lt = is_lds(u);
+      fetch(task_of(u), lt, lt ? tb : l2b, lt ? lbase : l2base);
+    };
     const uint32_t nu = nL + nR;
-    if (w < nu) fetch(task_of(w));
+    if (w < nu) fetch_u(w);
     for (uint32_t u = w; u < nu; u += nw) {
-      const uint32_t t = task_of(u);
-      (void)t;
+      const bool lds_task = is_lds(u);
       u32x4 cv[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) cv[q] = cn[q];
@@ -478,28 +499,32 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       if (A.dbg & 4u) b = 0;
       if (lane == 0) b |= 1u;  // a task always starts a piece
       // next task's stream words first: they stay in flight while this task gathers
-      if (u + nw < nu) fetch(task_of(u + nw));
-      // Sixteen gathers: a source inside the LDS block reads the LDS copy; the others are
-      // buffer loads issued back to back with EXEC cut to the lanes that need them (the
-      // address unit then spends no cycles on LDS lanes), then one wait for all of them.
-      // PAD_COL lanes fall outside the buffer range and read 0.
+      if (u + nw < nu) fetch_u(u + nw);
       double v[EPL];
-      uint32_t qo[EPL];
-      uint64_t gm[EPL];
+      if (lds_task) {
+        // every source of an LDS-group task is inside the block (padding reads the zero slot)
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        const uint32_t q = cv[k >> 2][k & 3] & cm;
-        const uint32_t o = q - hb;
-        const bool h = o < Hs;
-        v[k] = hot[h ? o : 0u];
-        qo[k] = q * 8u;
-        gm[k] = __ballot(!h);
-      }
-      if (A.dbg & 2u) {
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) v[k] = static_cast<double>(qo[k] & 0xFFFF);
+        for (int k = 0; k < EPL; ++k) {
+          const uint32_t wd = cv[k >> 3][(k >> 1) & 3];
+          v[k] = hot[(k & 1) ? (wd >> 16) : (wd & 0xFFFFu)];
+        }
       } else {
-        gather16(v, qo, gm, xr);
+        // sixteen buffer gathers issued back to back; PAD_COL lanes fall outside the buffer
+        // range and read 0
+        uint32_t qo[EPL];
+        uint64_t gm[EPL];
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) {
+          v[k] = 0.0;
+          qo[k] = (cv[k >> 2][k & 3] & cm) * 8u;
+          gm[k] = ~0ull;
+        }
+        if (A.dbg & 2u) {
+#pragma unroll
+          for (int k = 0; k < EPL; ++k) v[k] = static_cast<double>(qo[k] & 0xFFFF);
+        } else {
+          gather16(v, qo, gm, xr);
+        }
       }
     // exclusive prefix (over lanes) of the piece starts -> first piece index of this lane
     const int cnt = __popc(b);
@@ -909,25 +934,34 @@ __global__ void k_group_starts(const uint64_t* key, uint64_t n, StreamGeo G,
     atomicMin(&starts[gr], static_cast<unsigned long long>(e));
 }
 
-// col (x position) of every stream edge + the pair-start flags
+// column of every stream edge (LDS groups: u16 offset inside the block; L2 group: x position)
+// + the pair-start flags (indexed by global stream position = task * TASK + offset)
 __global__ void k_stream_fill(const uint64_t* key, uint64_t n, Layout L, StreamGeo G,
-                              const uint64_t* gstart, const uint32_t* gtask, uint32_t* col,
+                              const uint64_t* gstart, const uint32_t* gtask,
+                              const uint64_t* gbase, uint32_t* col, uint16_t* col16,
                               uint32_t* bits32, unsigned long long* n_pairs) {
   const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   bool start = false;
   if (e < n) {
     const uint64_t k = key[e];
     const uint32_t gr = group_of_key(G, k);
-    const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + (e - gstart[gr]);
+    const uint64_t rel = e - gstart[gr];
+    const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + rel;
     const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
     const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
     const uint32_t qin = static_cast<uint32_t>(k & ((1ull << G.qb) - 1));
-    col[pos] = xpos(L, col_of_slice_q(L, G, sl, q_of_seg(G, seg, qin)));
+    if (seg < G.nlds) col16[gbase[gr] + rel] = static_cast<uint16_t>(qin);
+    else col[gbase[gr] + rel] = xpos(L, col_of_slice_q(L, G, sl, q_of_seg(G, seg, qin)));
     start = e == gstart[gr] || (key[e - 1] >> G.qb) != (k >> G.qb);
     if (start) atomicOr(&bits32[pos / 32], 1u << (pos % 32));
   }
   const uint64_t s = wave_sum_u64(start ? 1u : 0u);
   if ((threadIdx.x & 63) == 0 && s) atomicAdd(n_pairs, static_cast<unsigned long long>(s));
+}
+
+__global__ void k_fill_u16(uint16_t* a, uint64_t n, uint16_t v) {
+  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  if (i < n) a[i] = v;
 }
 
 // pieces of each task (piece starts: the task's first edge and every pair start)
@@ -1028,10 +1062,11 @@ __global__ void k_piece_row_runs(const uint32_t* T, const uint16_t* roff, RowBlo
   const uint32_t r0 = block_row0(B, b);
   for (uint32_t i = T[t]; i < T[t + B.NS]; ++i) piece_row[i] = r0 + roff[i];
 }
-__global__ void k_export_keys(const uint32_t* col, const uint32_t* bits32,
+__global__ void k_export_keys(const uint32_t* col, const uint16_t* col16, const uint32_t* bits32,
                               const uint32_t* task_piece, const uint32_t* piece_row, Layout L,
-                              const uint64_t* gstart, const uint32_t* gtask, uint32_t ngroups,
-                              uint64_t stream_len, uint64_t* out) {
+                              const uint64_t* gstart, const uint32_t* gtask, const uint64_t* gbase,
+                              uint32_t ngroups, uint32_t nlds, uint32_t H, uint64_t stream_len,
+                              uint64_t* out) {
   const uint64_t pos = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
   if (pos >= stream_len) return;
   const uint32_t t = static_cast<uint32_t>(pos / TASK);
@@ -1044,7 +1079,11 @@ __global__ void k_export_keys(const uint32_t* col, const uint32_t* bits32,
   if (rel >= gstart[lo + 1] - gstart[lo]) return;  // padding
   const uint32_t pc = piece_of(bits32, task_piece, pos, nullptr);
   const uint32_t row = row_of(L, piece_row[pc]);
-  out[gstart[lo] + rel] = (static_cast<uint64_t>(row) << 32) | col_of_xpos(L, col[pos]);
+  const uint32_t j = lo / (nlds + 1), gi = lo % (nlds + 1);
+  uint32_t xp;
+  if (gi < nlds) xp = (j % L.p) * L.maxA + (j / L.p) * L.SL + gi * H + col16[gbase[lo] + rel];
+  else xp = col[gbase[lo] + rel];
+  out[gstart[lo] + rel] = (static_cast<uint64_t>(row) << 32) | col_of_xpos(L, xp);
 }
 __global__ void k_export_split(const uint64_t* key, uint64_t n, uint32_t* col, uint64_t* row_ptr) {
   const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
@@ -1116,7 +1155,7 @@ int env_int(const char* name, int def) {
 void dev_free(DevGraph* g) {
   auto F = [](void* p) { if (p) (void)hipFree(p); };
   F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->roff); F(g->runs);
-  F(g->d_gtask); F(g->d_gstart);
+  F(g->d_gtask); F(g->d_gstart); F(g->d_gbase); F(g->col16);
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
   F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state);
@@ -1397,13 +1436,29 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   HIPTRY(hipMemcpyAsync(g->d_gtask, g->gtask.data(), 4ull * (NG + 1), hipMemcpyHostToDevice, s));
   HIPTRY(hipMemcpyAsync(g->d_gstart, g->gstart.data(), 8ull * (NG + 1), hipMemcpyHostToDevice, s));
 
-  // ---- stream arrays: col, pair-start flags, pieces ------------------------------------------
-  TRY(dmalloc(&g->col, g->stream_len, err));
+  // ---- stream arrays: columns (u16 for LDS groups, u32 for the L2 group), flags, pieces --------
+  {
+    g->gbase.assign(NG + 1, 0);
+    uint64_t n16 = 0, n32 = 0;
+    for (uint32_t i = 0; i < NG; ++i) {
+      const uint64_t len = static_cast<uint64_t>(g->gtask[i + 1] - g->gtask[i]) * TASK;
+      const bool lds_group = (i % (G.nlds + 1)) < G.nlds;
+      g->gbase[i] = lds_group ? n16 : n32;
+      (lds_group ? n16 : n32) += len;
+    }
+    g->n_col16 = n16;
+    g->n_col32 = n32;
+  }
+  TRY(dmalloc(&g->d_gbase, NG + 1ull, err));
+  HIPTRY(hipMemcpyAsync(g->d_gbase, g->gbase.data(), 8ull * (NG + 1), hipMemcpyHostToDevice, s));
+  TRY(dmalloc(&g->col, g->n_col32, err));
+  TRY(dmalloc(&g->col16, g->n_col16, err));
   TRY(dmalloc(&g->bits, g->stream_len / EPL + 2, err));
-  HIPTRY(hipMemsetAsync(g->col, 0xFF, 4 * std::max<uint64_t>(g->stream_len, 1), s));  // PAD_COL
+  HIPTRY(hipMemsetAsync(g->col, 0xFF, 4 * std::max<uint64_t>(g->n_col32, 1), s));  // PAD_COL
+  if (g->n_col16) hipLaunchKernelGGL(k_fill_u16, dim3(grid_for(g->n_col16)), dim3(BLOCK), 0, s, g->col16, g->n_col16, static_cast<uint16_t>(G.H));  // zero slot
   HIPTRY(hipMemsetAsync(g->bits, 0, 2 * (g->stream_len / EPL + 2), s));
   uint32_t* bits32 = reinterpret_cast<uint32_t*>(g->bits);
-  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, g->d_gstart, g->d_gtask, g->col, bits32, d_cnt + 1);
+  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, g->d_gstart, g->d_gtask, g->d_gbase, g->col, g->col16, bits32, d_cnt + 1);
   TRY(dmalloc(&g->task_piece, tasks + 1ull, err));
   {
     uint32_t* tcnt = nullptr;
@@ -1516,7 +1571,7 @@ double* dev_x_out(DevGraph* g, int t) { return g->xbuf[(t - 1) & 1]; }
 namespace {
 
 void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
-  const size_t lds = 8ull * ((A.nlds ? A.H : 0u) + (STREAM_BLOCK / 64) * STG);
+  const size_t lds = 8ull * ((A.nlds ? A.H + 8u : 0u) + (STREAM_BLOCK / 64) * STG);
   // persistent grid: 32 CUs per XCD, one 1024-thread block per CU (the LDS holds one x
   // block + the staging windows); PR_STREAM_WG blocks per CU without LDS blocks
   const int per_cu = A.nlds ? 1 : std::max(1, g->tune.stream_wg);
@@ -1540,6 +1595,8 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   const double* x_in = t == 1 ? g->x_init : g->xbuf[t & 1];
   StreamArgs S{};
   S.col = g->col;
+  S.col16 = g->col16;
+  S.gbase = g->d_gbase;
   S.bits = g->bits;
   S.task_piece = g->task_piece;
   S.gtask = g->d_gtask;
@@ -1626,7 +1683,7 @@ int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s,
   TRY(dmalloc(&c, m, err)); fr.v.push_back(c);
   const RowBlocks RBk{g->lA, g->nb_rows_a, g->nb_rows, g->n_streams};
   if (g->nb_rows) hipLaunchKernelGGL(k_piece_row_runs, dim3(grid_for(static_cast<uint64_t>(g->nb_rows) * g->n_streams)), dim3(BLOCK), 0, s, g->runs, g->roff, RBk, prow);
-  if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_for(g->stream_len)), dim3(BLOCK), 0, s, g->col, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, g->d_gstart, g->d_gtask, static_cast<uint32_t>(g->gtask.size() - 1), g->stream_len, k0);
+  if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_for(g->stream_len)), dim3(BLOCK), 0, s, g->col, g->col16, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, g->d_gstart, g->d_gtask, g->d_gbase, static_cast<uint32_t>(g->gtask.size() - 1), g->nlds, g->hot_h, g->stream_len, k0);
   rocprim::double_buffer<uint64_t> db(k0, k1);
   size_t tb = 0;
   HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, m, 0, 64, s));
