@@ -124,8 +124,8 @@ def main():
     n = int(info["n_vertices"])
     gteps = nnz / (ms_step * 1e-3) / 1e9
     workload = f"rmat-s{a.scale}-ef{a.edge_factor}"
-    # roofline of the dominant kernel pair (XCD-sliced partials + row launch, bracketed by HIP
-    # events on the engine stream): SURVEY.md 8d algorithmic bytes, this rank's share
+    # roofline of the SpMV of one round (stream launch + row launch, bracketed by HIP events on
+    # the engine stream): SURVEY.md 8d algorithmic bytes, this rank's share
     local_nnz = int(info["local_nnz"])
     bytes_launch = 4 * local_nnz + 24 * n // world + 8
     kms = st["ms_spmv_kernel"]
@@ -156,7 +156,7 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "spmv_slices+spmv_round (the SpMV of one round)",
+                         "kernel": "spmv_stream+spmv_rows (the SpMV of one round)",
                          "kernel_ms": round(kms, 4),
                          "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,

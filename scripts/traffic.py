@@ -24,19 +24,19 @@ def load(name):
 
 def per_round(agg, ctr):
     """sum over the SpMV kernels of one round (mean per dispatch of each kernel, summed
-    over the distinct kernels that run once per round: slice launch + row launch)."""
+    over the distinct kernels that run once per round: stream launch + row launch)."""
     tot = 0.0
     for k, cs in agg.items():
-        if ctr in cs and ("spmv_round" in k or "spmv_slices" in k):
+        if ctr in cs and ("spmv_stream" in k or "spmv_rows" in k):
             tot += sum(cs[ctr]) / len(cs[ctr])
     return tot
 
 
 rd, wr, fe, ws, l2 = (load(x) for x in ("rd", "wr", "fetch", "write", "l2"))
-# spmv_round<0> (plain rounds) and <1> (last round) both appear: keep one row-launch variant
+# spmv_rows<0> (plain rounds) and <1> (last round) both appear: keep one row-launch variant
 for agg in (rd, wr, fe, ws, l2):
     for k in list(agg):
-        if "spmv_round<1" in k:
+        if "spmv_rows<1" in k or "spmv_rows<2" in k:
             del agg[k]
 read_b = (per_round(rd, "TCC_EA0_RDREQ_32B_sum") * 32 + per_round(rd, "TCC_EA0_RDREQ_64B_sum") * 64
           + per_round(rd, "TCC_EA0_RDREQ_128B_sum") * 128)
@@ -48,7 +48,7 @@ entry = {
     "fetch_size_x1024": per_round(fe, "FETCH_SIZE") * 1024,
     "write_size_x1024": per_round(ws, "WRITE_SIZE") * 1024,
     "l2_hit": per_round(l2, "TCC_HIT_sum"), "l2_miss": per_round(l2, "TCC_MISS_sum"),
-    "note": "per round = one spmv_slices + one spmv_round launch; rocprofv3 PMC passes",
+    "note": "per round = one spmv_stream + one spmv_rows launch; rocprofv3 PMC passes",
 }
 cur = json.load(open(dst)) if os.path.exists(dst) else {}
 cur[key] = entry
