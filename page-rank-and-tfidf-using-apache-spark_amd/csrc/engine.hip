@@ -292,9 +292,17 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   double* aw = acc[wv];
   uint32_t kw = 0;  // wave-uniform lower bound of the stream search
   for (uint32_t pos = lo; pos < hi; pos += 64 * EPR) {
-    const uint32_t i0 = pos + lane * EPR;
-    // stream of i0: last k with pre[k] <= i0 (empty streams share pre with the next one)
-    uint32_t k = kw, kh = NS - 1;
+    // lane l takes pieces pos + l + 64u: the lanes of one load cover 64 consecutive pieces
+    // (one coalesced 512-B read inside a long run)
+    const uint32_t i0 = pos + lane;
+    // stream of i0: last k with pre[k] <= i0 (empty streams share pre with the next one);
+    // galloping search from the wave's lower bound
+    uint32_t k = kw, stp = 1;
+    while (k + stp < NS && pre[k + stp] <= i0) {
+      k += stp;
+      stp <<= 1;
+    }
+    uint32_t kh = min(k + stp, NS) - 1;
     while (k < kh) {
       const uint32_t mid = (k + kh + 1) >> 1;
       if (pre[mid] <= i0) k = mid; else kh = mid - 1;
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     uint32_t pc[EPR];
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
-      const uint32_t i = i0 + u;
+      const uint32_t i = i0 + 64u * u;
       while (k + 1 < NS && pre[k + 1] <= i) ++k;
       pc[u] = i < hi ? st[k] + (i - pre[k]) : 0u;  // never address past the pieces
     }
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     uint32_t r[EPR];
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
-      const bool ok = i0 + u < hi;
+      const bool ok = i0 + 64u * u < hi;
       val[u] = A.partial[pc[u]];
       r[u] = A.roff[pc[u]];
       if (!ok) val[u] = 0.0;
@@ -318,7 +326,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     // LDS adds in lane order inside each instruction: a fixed order for a fixed layout
 #pragma unroll
     for (int u = 0; u < EPR; ++u)
-      if (i0 + u < hi) atomicAdd(&aw[r[u]], val[u]);
+      if (i0 + 64u * u < hi) atomicAdd(&aw[r[u]], val[u]);
     kw = __builtin_amdgcn_readfirstlane(k);  // lane 0's stream after this step (monotone)
   }
   __syncthreads();
