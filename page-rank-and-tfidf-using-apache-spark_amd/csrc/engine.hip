@@ -374,6 +374,56 @@ constexpr uint32_t HOT_MAX = 20480 - (STREAM_BLOCK / 64) * STG - 8;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// ---- DPP cross-lane steps (gfx9 wave64: row shifts, row broadcasts, wave shifts) ----------
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114,
+              DPP_ROW_SHR8 = 0x118, DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143,
+              DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138;
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);  // invalid source -> 0
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t u = static_cast<uint64_t>(__double_as_longlong(v));
+  const uint32_t lo = static_cast<uint32_t>(dpp_i<CTRL>(static_cast<int>(u)));
+  const uint32_t hi = static_cast<uint32_t>(dpp_i<CTRL>(static_cast<int>(u >> 32)));
+  return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
+}
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+  const int rl = lane & 15;
+  int t;
+  t = dpp_i<DPP_ROW_SHR1>(v); if (rl >= 1) v += t;
+  t = dpp_i<DPP_ROW_SHR2>(v); if (rl >= 2) v += t;
+  t = dpp_i<DPP_ROW_SHR4>(v); if (rl >= 4) v += t;
+  t = dpp_i<DPP_ROW_SHR8>(v); if (rl >= 8) v += t;
+  t = dpp_i<DPP_ROW_BCAST15>(v); if (lane & 16) v += t;   // rows 1, 3 add lanes 15, 47
+  t = dpp_i<DPP_ROW_BCAST31>(v); if (lane >= 32) v += t;  // rows 2, 3 add lane 31
+  return v;
+}
+// segmented inclusive scan: (F, S) o (F', S') = (F | F', F' ? S' : S + S'), F = lane starts a
+// segment; the same fixed combination tree for a given flag pattern
+__device__ __forceinline__ double wave_seg_scan(double S, int F, int lane) {
+  const int rl = lane & 15;
+  double Su;
+  int Fu;
+#define PRMI_SEG_STEP(CTRL, COND)          \
+  Su = dpp_d<CTRL>(S);                     \
+  Fu = dpp_i<CTRL>(F);                     \
+  if (COND) {                              \
+    if (!F) S = Su + S;                    \
+    F |= Fu;                               \
+  }
+  PRMI_SEG_STEP(DPP_ROW_SHR1, rl >= 1)
+  PRMI_SEG_STEP(DPP_ROW_SHR2, rl >= 2)
+  PRMI_SEG_STEP(DPP_ROW_SHR4, rl >= 4)
+  PRMI_SEG_STEP(DPP_ROW_SHR8, rl >= 8)
+  PRMI_SEG_STEP(DPP_ROW_BCAST15, (lane & 16) != 0)
+  PRMI_SEG_STEP(DPP_ROW_BCAST31, lane >= 32)
+#undef PRMI_SEG_STEP
+  return S;
+}
+
 // Sixteen exec-masked buffer gathers x[off/8] into v[k] (lanes outside gm[k] keep v[k]),
 // then one s_waitcnt: the asm block ends with its loads landed, so the compiler never sees
 // an in-flight destination.
@@ -536,14 +586,9 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       }
     // exclusive prefix (over lanes) of the piece starts -> first piece index of this lane
     const int cnt = __popc(b);
-    int C = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(C, d);
-      if (lane >= d) C += y;
-    }
+    const int C = wave_incl_scan(cnt, lane);
     const uint32_t first = static_cast<uint32_t>(C - cnt);  // task-relative index of the lane's first start
-    const uint32_t total = static_cast<uint32_t>(__shfl(C, 63));  // pieces of the task
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(C, 63));  // pieces of the task
     // the lane's head (edges before its first start) and its open piece
     double run = 0.0, head = 0.0;
     {
@@ -559,19 +604,9 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       }
     }
     // segmented inclusive scan of the open piece over lanes (flag: lane holds a start)
-    double S = run;
-    bool F = b != 0u;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const double Su = __shfl_up(S, d);
-      const int Fu = __shfl_up(static_cast<int>(F), d);
-      if (lane >= d) {
-        if (!F) S = Su + S;
-        F = F || Fu != 0;
-      }
-    }
-    const double carry = __shfl_up(S, 1);
-    const uint32_t bn = __shfl_down(b, 1);
+    const double S = wave_seg_scan(run, b != 0u ? 1 : 0, lane);
+    const double carry = dpp_d<DPP_WAVE_SHR1>(S);
+    const uint32_t bn = static_cast<uint32_t>(dpp_i<DPP_WAVE_SHL1>(static_cast<int>(b)));
     const bool closes = lane == 63 || (bn & 1u) != 0u;  // next edge starts a piece
     // Pieces go to the wave's LDS staging window (STG pieces at a time) and leave it as
     // contiguous 512-byte stores: one L2 request per line instead of one per piece.
