@@ -368,7 +368,7 @@ struct StreamArgs {
                              // and PAD_COL padding)
 };
 constexpr int STREAM_BLOCK = 1024;
-constexpr int STG = 128;           // per-wave LDS staging window for piece stores (doubles)
+constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
 // LDS left for the x block: H entries + a zero slot (index H, the 16-bit padding column)
 constexpr uint32_t HOT_MAX = 20480 - (STREAM_BLOCK / 64) * STG - 8;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
