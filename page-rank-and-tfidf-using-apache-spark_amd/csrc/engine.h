@@ -52,7 +52,7 @@ struct IterState {
 
 struct Tuning {
   uint32_t qh = 458752; // PR_QH: L2-hot segment length per slice after the LDS blocks (3.5 MiB)
-  int nlds = 12;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
+  int nlds = 16;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
   int nt = 0;           // PR_NT: non-temporal loads for the streamed arrays (slower: 3.8 vs 6 TB/s)
   uint32_t hot_lds = 20480;  // PR_HOTLDS: LDS block length (x entries, capped by the staging room)
