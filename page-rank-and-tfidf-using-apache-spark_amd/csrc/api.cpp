@@ -89,7 +89,7 @@ int build_device(pr_ctx* c, const prmi::BuildInput& in) {
   if (rc) return fail(c, rc, "device build: " + e);
   c->last_iters = -1;
   c->host_ranks_valid = false;
-  if (c->opts.flags & PR_F_VERBOSE)
+  if ((c->opts.flags & PR_F_VERBOSE) || getenv("PR_VERBOSE"))
     fprintf(stderr, "[prmi355x] rank %d build %.1f ms: n=%u nnz=%llu rows=%u local_rows=%u local_nnz=%llu segments/slice=%u pairs=%llu pieces=%llu tasks=%u streams=%zu row_blocks=%u\n",
             c->opts.rank, c->dg.ms_build, c->dg.n, (unsigned long long)c->dg.nnz, c->dg.R,
             c->dg.lrows, (unsigned long long)c->dg.lnnz, c->dg.nseg,
