@@ -285,3 +285,67 @@ def test_rank_group_text_and_errors(P, O):
     bad.each("ingest_buffers", b"1\t2\n1\t3\n2\t3\n3\t1\n4\t3\n", b"1\tA\n2\tB\n3\tC\n4\tD\n5\tE\n")
     with pytest.raises(P.UnsupportedOperationException, match="iteration 2"):
         bad.run(5)
+
+
+# ---- the stream layout at small scale: tiny LDS blocks / segments force every code path ----
+@pytest.fixture
+def tiny_blocks(monkeypatch):
+    """LDS blocks of 256 x entries, a 1024-entry L2-hot range and 512-entry cold segments:
+    small graphs then use LDS groups (16-bit columns), the L2 group, cold segments and
+    group padding, which the default sizes only reach at scale >= 18."""
+    for k, v in (("PR_HOTLDS", "256"), ("PR_NLDS", "6"), ("PR_QH", "1024"), ("PR_SEG", "512")):
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("scale,ef,seed", [(14, 16, 21), (16, 8, 22)])
+def test_stream_layout_tiny_blocks(P, O, tiny_blocks, scale, ef, seed):
+    g = O.Graph.from_rmat(scale, ef, seed)
+    exp = g.run(10)["ranks"]
+    eng = P.Engine()
+    eng.generate_rmat(scale, ef, seed)
+    eng.run(10)
+    parity.assert_ranks_close(eng.ranks(), exp)
+    for p in (2, 3):   # slice-major (p | 8) and plain x layouts
+        grp = P.LocalGroup(p)
+        grp.each("generate_rmat", scale, ef, seed)
+        grp.run(10)
+        parity.assert_ranks_close(grp.members[0].ranks(), exp)
+        grp.close()
+
+
+def test_export_csr_is_the_same_graph(P, O):
+    """pr_export_csr rebuilds the pull CSR from the streams (internal ids): the oracle run on
+    it gives the engine's rank multiset, and its degrees match the edge set."""
+    eng = P.Engine()
+    eng.generate_rmat(15, 16, 7)
+    eng.run(10)
+    got = np.sort(eng.ranks())
+    rp, col, od, dw = eng.export_csr()
+    n = len(od)
+    assert int(rp[-1]) == eng.info()["nnz"] == len(col)
+    assert np.all(np.diff(rp.astype(np.int64)) >= 0)
+    indeg = np.diff(rp.astype(np.int64))
+    g = O.Graph.from_rmat(15, 16, 7)
+    eo, ei, ew = g.degrees()
+    assert np.array_equal(np.sort(indeg), np.sort(ei.astype(np.int64)))
+    assert np.array_equal(np.bincount(col, minlength=n), od.astype(np.int64))
+    for r in range(0, n, max(1, n // 97)):          # sources ascending inside each row
+        seg = col[rp[r]:rp[r + 1]]
+        assert np.all(np.diff(seg.astype(np.int64)) > 0)
+    res = O.pagerank_csr(rp, col, od, dw, int(eng.info()["n_tot"]), 10, exact=True)
+    parity.assert_ranks_close(got, np.sort(res["ranks"]))
+
+
+def test_rank_sum_checksum_scale22(P):
+    """Size-independent property at a large graph: the exact rank sum the engine accumulates
+    in tracked mode (integer superaccumulator, one rounding) equals the correctly rounded
+    exact sum of the ranks it returns."""
+    import math
+    eng = P.Engine()
+    eng.generate_rmat(22, 16, 8)
+    st = eng.run(10, 1e-300)           # tol > 0: tracked mode, all 10 rounds run
+    assert st["iterations"] == 10
+    r = eng.ranks()
+    assert st["rank_sum"] == math.fsum(r.tolist())
+    d = r > 0
+    assert d.sum() > 0 and np.all(r[d] >= 0.15)
