@@ -589,20 +589,29 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     const int C = wave_incl_scan(cnt, lane);
     const uint32_t first = static_cast<uint32_t>(C - cnt);  // task-relative index of the lane's first start
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(C, 63));  // pieces of the task
-    // the lane's head (edges before its first start) and its open piece
+    // one pass over the lane's edges: the head (edges before its first start), the open piece,
+    // and pv[k] = the piece that closes just before edge k (static slots: no scratch)
     double run = 0.0, head = 0.0;
+    double pv[EPL];
     {
       bool ih = (b & 1u) == 0u;
 #pragma unroll
       for (int k = 0; k < EPL; ++k) {
+        pv[k] = 0.0;
         if ((b >> k) & 1u) {
-          if (k > 0 && ih) head = run;
+          if (k > 0) {
+            if (ih) head = run;
+            else pv[k] = run;
+          }
           ih = false;
           run = 0.0;
         }
         run += v[k];
       }
     }
+    // slot k holds a middle piece when edge k starts one and it is not the head's end
+    const uint32_t k0 = b ? static_cast<uint32_t>(__builtin_ctz(b)) : 32u;
+    const uint32_t mids = (b & ~1u) & ~((b & 1u) ? 0u : (1u << k0));
     // segmented inclusive scan of the open piece over lanes (flag: lane holds a start)
     const double S = wave_seg_scan(run, b != 0u ? 1 : 0, lane);
     const double carry = dpp_d<DPP_WAVE_SHR1>(S);
@@ -616,21 +625,10 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
         if (r - w0 < wn) stg[r - w0] = val;
       };
       if (first + cnt > w0 && first < w0 + wn + 1u) {
-        uint32_t r = first - 1u;  // relative index of the piece open before edge 0
-        double rr = 0.0;
-        bool ih = (b & 1u) == 0u;
 #pragma unroll
-        for (int k = 0; k < EPL; ++k) {
-          if ((b >> k) & 1u) {
-            if (k > 0) {
-              if (!ih) put(r, rr);  // a piece that starts and ends inside the lane
-              ih = false;
-            }
-            ++r;
-            rr = 0.0;
-          }
-          rr += v[k];
-        }
+        for (int k = 1; k < EPL; ++k)
+          if ((mids >> k) & 1u)  // piece index: first - 1 + starts before edge k
+            put(first - 1u + static_cast<uint32_t>(__popc(b & ((1u << k) - 1u))), pv[k]);
         if (b == 0u) {
           if (closes) put(first - 1u, S);            // lane inside a longer piece
         } else {
