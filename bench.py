@@ -136,7 +136,7 @@ def main():
         cpu = cpu_baseline(eng, a.cpu_rounds)
     if rank == 0:
         line = {
-            "metric": "PageRank GTEPS per round (distinct edges / round time), R-MAT scale-26",
+            "metric": f"PageRank GTEPS per round (distinct edges / round time), R-MAT scale-{a.scale}",
             "value": round(gteps, 3),
             "unit": "GTEPS",
             "n_gpus": world,

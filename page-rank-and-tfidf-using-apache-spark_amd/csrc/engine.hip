@@ -165,7 +165,8 @@ __device__ double sa_to_double_dev(const uint64_t* limb) {
 // accumulator; c[row] = (acc0 + acc1) + (acc2 + acc3).  Then PageRank.java's damping /
 // contribution epilogue.
 constexpr int RB = 1024;           // rows per row-launch block
-constexpr int MAX_NS = 512;        // streams (slices x segments) the row launch supports
+constexpr int MAX_NS = 1024;       // streams (slices x segments) the row launch supports
+// (NSC = 512 or 1024 stream capacity: the small one keeps four workgroups per CU)
 constexpr int EPR = 8;             // pieces per lane per step (16 measured slower)
 struct RowArgs {
   const uint32_t* T;       // [(NB + 1) * NS] run starts
@@ -248,29 +249,32 @@ __device__ __forceinline__ void row_epilogue(const RowArgs& A, double a, uint32_
 
 // The row launch (PageRank.java:139-145 reduceByKey(Sum) + mapValues, and the inputs of
 // :113 and :125-134 for the next round).
-template <int MODE>
+template <int MODE, int NSC>
 __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
+  constexpr int SPT = NSC / BLOCK;  // streams per thread in the run prefix
   __shared__ double acc[4][RB];
-  __shared__ uint32_t pre[MAX_NS + 1], st[MAX_NS];
+  __shared__ uint32_t pre[NSC + 1], st[NSC];
   __shared__ uint32_t wtot[4];
   __shared__ uint64_t lds[4][REC_WORDS];
   const uint32_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < 4 * RB; i += BLOCK) (&acc[0][0])[i] = 0.0;
-  // run lengths of the block's streams -> exclusive prefix pre[] (two streams per thread)
+  // run lengths of the block's streams -> exclusive prefix pre[] (SPT streams per thread)
   const uint32_t NS = A.NS;
   const uint32_t* T0 = A.T + static_cast<uint64_t>(b) * NS;
-  const uint32_t k0 = 2 * tid, k1 = 2 * tid + 1;
-  uint32_t len0 = 0, len1 = 0;
-  if (k0 < NS) {
-    st[k0] = T0[k0];
-    len0 = T0[NS + k0] - T0[k0];
+  uint32_t len[SPT];
+  uint32_t inc = 0;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const uint32_t k = SPT * tid + q;
+    len[q] = 0;
+    if (k < NS) {
+      st[k] = T0[k];
+      len[q] = T0[NS + k] - T0[k];
+    }
+    inc += len[q];
   }
-  if (k1 < NS) {
-    st[k1] = T0[k1];
-    len1 = T0[NS + k1] - T0[k1];
-  }
-  uint32_t inc = len0 + len1;
+  const uint32_t mine = inc;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(inc, d);
@@ -280,9 +284,13 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   __syncthreads();
   uint32_t base = 0;
   for (int i = 0; i < wv; ++i) base += wtot[i];
-  const uint32_t ex = base + inc - len0 - len1;
-  if (k0 < NS) pre[k0] = ex;
-  if (k1 < NS) pre[k1] = ex + len0;
+  uint32_t ex = base + inc - mine;
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const uint32_t k = SPT * tid + q;
+    if (k < NS) pre[k] = ex;
+    ex += len[q];
+  }
   if (tid == 0) pre[NS] = wtot[0] + wtot[1] + wtot[2] + wtot[3];
   __syncthreads();
   // this wave's quarter of the concatenated runs, EPR consecutive pieces per lane per step
@@ -700,6 +708,12 @@ __global__ void finalize_round(const uint64_t* rec_all, int p, int t, uint64_t n
   st->iter = t;
 }
 
+// Large launches (edge counts reach 2^32 at R-MAT scale 28) loop over blocks: every thread of
+// a block runs the same iterations, so block- and wave-level operations in the body stay
+// uniform, and the grid stays far below the 2^32 work-item limit.
+#define PRMI_BLOCK_LOOP(n) \
+  for (uint64_t blk_ = blockIdx.x; blk_ * blockDim.x < (n); blk_ += gridDim.x)
+
 // =======================================================================================
 // graph build (K1): keys -> sort -> unique -> degrees -> vertex order -> local CSR
 // =======================================================================================
@@ -724,64 +738,71 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
 constexpr uint32_t kRmatA = 2448131358u, kRmatAB = 3264175144u, kRmatABC = 4080218931u;
 
 __global__ void k_rmat_keys(uint64_t seed, int scale, uint64_t m, uint64_t* keys) {
-  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (e >= m) return;
-  uint32_t s = 0, d = 0, w[4] = {0, 0, 0, 0};
-  for (int lv = 0; lv < scale; ++lv) {
-    if ((lv & 3) == 0) {
-      w[0] = static_cast<uint32_t>(e);
-      w[1] = static_cast<uint32_t>(e >> 32);
-      w[2] = static_cast<uint32_t>(lv >> 2);
-      w[3] = 0x524D4154u;  // "RMAT"
-      philox4x32_10(w, static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+  PRMI_BLOCK_LOOP(m) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    if (e >= m) continue;
+    uint32_t s = 0, d = 0, w[4] = {0, 0, 0, 0};
+    for (int lv = 0; lv < scale; ++lv) {
+      if ((lv & 3) == 0) {
+        w[0] = static_cast<uint32_t>(e);
+        w[1] = static_cast<uint32_t>(e >> 32);
+        w[2] = static_cast<uint32_t>(lv >> 2);
+        w[3] = 0x524D4154u;  // "RMAT"
+        philox4x32_10(w, static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+      }
+      const uint32_t u = w[lv & 3];
+      const uint32_t sb = u >= kRmatAB;
+      const uint32_t db = (u >= kRmatA && u < kRmatAB) || u >= kRmatABC;
+      s = (s << 1) | sb;
+      d = (d << 1) | db;
     }
-    const uint32_t u = w[lv & 3];
-    const uint32_t sb = u >= kRmatAB;
-    const uint32_t db = (u >= kRmatA && u < kRmatAB) || u >= kRmatABC;
-    s = (s << 1) | sb;
-    d = (d << 1) | db;
+    keys[e] = (static_cast<uint64_t>(d) << scale) | s;
   }
-  keys[e] = (static_cast<uint64_t>(d) << scale) | s;
 }
 
 __global__ void k_make_keys(const uint32_t* src, const uint32_t* dst, uint64_t m, int nb,
                             uint64_t* keys) {
-  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (e < m) keys[e] = (static_cast<uint64_t>(dst[e]) << nb) | src[e];
+  PRMI_BLOCK_LOOP(m) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    if (e < m) keys[e] = (static_cast<uint64_t>(dst[e]) << nb) | src[e];
+  }
 }
 
 __global__ void k_degrees(const uint64_t* uk, uint64_t nnz, int nb, uint32_t* outdeg,
                           uint32_t* indeg, unsigned long long* digest) {
   __shared__ unsigned long long ssum[BLOCK / 64], sxor[BLOCK / 64];
-  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  uint64_t h = 0;
-  if (e < nnz) {
-    const uint64_t k = uk[e];
-    const uint32_t d = static_cast<uint32_t>(k >> nb);
-    const uint32_t s = static_cast<uint32_t>(k & ((1ull << nb) - 1));
-    atomicAdd(&outdeg[s], 1u);
-    atomicAdd(&indeg[d], 1u);
-    h = mix64((static_cast<uint64_t>(s) << 32) | d);
-  }
-  uint64_t hs = h, hx = h;
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    hs += __shfl_xor(hs, m);
-    hx ^= __shfl_xor(hx, m);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    ssum[threadIdx.x >> 6] = hs;
-    sxor[threadIdx.x >> 6] = hx;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long a = 0, x = 0;
-    for (int i = 0; i < BLOCK / 64; ++i) {
-      a += ssum[i];
-      x ^= sxor[i];
+  PRMI_BLOCK_LOOP(nnz) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    uint64_t h = 0;
+    if (e < nnz) {
+      const uint64_t k = uk[e];
+      const uint32_t d = static_cast<uint32_t>(k >> nb);
+      const uint32_t s = static_cast<uint32_t>(k & ((1ull << nb) - 1));
+      atomicAdd(&outdeg[s], 1u);
+      atomicAdd(&indeg[d], 1u);
+      h = mix64((static_cast<uint64_t>(s) << 32) | d);
     }
-    atomicAdd(&digest[0], a);
-    atomicXor(&digest[1], x);
+    uint64_t hs = h, hx = h;
+  #pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      hs += __shfl_xor(hs, m);
+      hx ^= __shfl_xor(hx, m);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      ssum[threadIdx.x >> 6] = hs;
+      sxor[threadIdx.x >> 6] = hx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long a = 0, x = 0;
+      for (int i = 0; i < BLOCK / 64; ++i) {
+        a += ssum[i];
+        x ^= sxor[i];
+      }
+      atomicAdd(&digest[0], a);
+      atomicXor(&digest[1], x);
+    }
+    __syncthreads();  // the next iteration reuses the shared partials
   }
 }
 
@@ -936,43 +957,47 @@ __device__ __forceinline__ uint32_t col_of_xpos(const Layout& L, uint32_t x) {
 // this rank's rows (wave-aggregated append when p > 1)
 __global__ void k_stream_keys(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv,
                               Layout L, StreamGeo G, unsigned long long* counter, uint64_t* out) {
-  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  bool keep = false;
-  uint64_t key = 0;
-  if (e < nnz) {
-    const uint64_t k = uk[e];
-    const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
-    const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
-    keep = owner_of(L, kd) == L.rank;
-    uint32_t sl, q, seg, qin;
-    col_slice_q(L, G, ks, sl, q);
-    seg_of_q(G, q, seg, qin);
-    key = (static_cast<uint64_t>(sl) << (G.sgb + G.rb + G.qb)) |
-          (static_cast<uint64_t>(seg) << (G.rb + G.qb)) |
-          (static_cast<uint64_t>(local_of(L, kd)) << G.qb) | qin;
+  PRMI_BLOCK_LOOP(nnz) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    bool keep = false;
+    uint64_t key = 0;
+    if (e < nnz) {
+      const uint64_t k = uk[e];
+      const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
+      const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
+      keep = owner_of(L, kd) == L.rank;
+      uint32_t sl, q, seg, qin;
+      col_slice_q(L, G, ks, sl, q);
+      seg_of_q(G, q, seg, qin);
+      key = (static_cast<uint64_t>(sl) << (G.sgb + G.rb + G.qb)) |
+            (static_cast<uint64_t>(seg) << (G.rb + G.qb)) |
+            (static_cast<uint64_t>(local_of(L, kd)) << G.qb) | qin;
+    }
+    if (L.p == 1) {
+      if (e < nnz) out[e] = key;
+      continue;
+    }
+    const uint64_t mask = __ballot(keep);
+    if (!mask) continue;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(counter, static_cast<unsigned long long>(__popcll(mask)));
+    base = __shfl(base, leader);
+    if (keep) out[base + __popcll(mask & ((1ull << lane) - 1))] = key;
   }
-  if (L.p == 1) {
-    if (e < nnz) out[e] = key;
-    return;
-  }
-  const uint64_t mask = __ballot(keep);
-  if (!mask) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll(static_cast<long long>(mask)) - 1;
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(counter, static_cast<unsigned long long>(__popcll(mask)));
-  base = __shfl(base, leader);
-  if (keep) out[base + __popcll(mask & ((1ull << lane) - 1))] = key;
 }
 
 // first sorted edge of each stream group (atomicMin; empty groups keep the sentinel)
 __global__ void k_group_starts(const uint64_t* key, uint64_t n, StreamGeo G,
                                unsigned long long* starts) {
-  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (e >= n) return;
-  const uint32_t gr = group_of_key(G, key[e]);
-  if (e == 0 || group_of_key(G, key[e - 1]) != gr)
-    atomicMin(&starts[gr], static_cast<unsigned long long>(e));
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    if (e >= n) continue;
+    const uint32_t gr = group_of_key(G, key[e]);
+    if (e == 0 || group_of_key(G, key[e - 1]) != gr)
+      atomicMin(&starts[gr], static_cast<unsigned long long>(e));
+  }
 }
 
 // column of every stream edge (LDS groups: u16 offset inside the block; L2 group: x position)
@@ -981,28 +1006,32 @@ __global__ void k_stream_fill(const uint64_t* key, uint64_t n, Layout L, StreamG
                               const uint64_t* gstart, const uint32_t* gtask,
                               const uint64_t* gbase, uint32_t* col, uint16_t* col16,
                               uint32_t* bits32, unsigned long long* n_pairs) {
-  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  bool start = false;
-  if (e < n) {
-    const uint64_t k = key[e];
-    const uint32_t gr = group_of_key(G, k);
-    const uint64_t rel = e - gstart[gr];
-    const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + rel;
-    const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
-    const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
-    const uint32_t qin = static_cast<uint32_t>(k & ((1ull << G.qb) - 1));
-    if (seg < G.nlds) col16[gbase[gr] + rel] = static_cast<uint16_t>(qin);
-    else col[gbase[gr] + rel] = xpos(L, col_of_slice_q(L, G, sl, q_of_seg(G, seg, qin)));
-    start = e == gstart[gr] || (key[e - 1] >> G.qb) != (k >> G.qb);
-    if (start) atomicOr(&bits32[pos / 32], 1u << (pos % 32));
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    bool start = false;
+    if (e < n) {
+      const uint64_t k = key[e];
+      const uint32_t gr = group_of_key(G, k);
+      const uint64_t rel = e - gstart[gr];
+      const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + rel;
+      const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
+      const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
+      const uint32_t qin = static_cast<uint32_t>(k & ((1ull << G.qb) - 1));
+      if (seg < G.nlds) col16[gbase[gr] + rel] = static_cast<uint16_t>(qin);
+      else col[gbase[gr] + rel] = xpos(L, col_of_slice_q(L, G, sl, q_of_seg(G, seg, qin)));
+      start = e == gstart[gr] || (key[e - 1] >> G.qb) != (k >> G.qb);
+      if (start) atomicOr(&bits32[pos / 32], 1u << (pos % 32));
+    }
+    const uint64_t s = wave_sum_u64(start ? 1u : 0u);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(n_pairs, static_cast<unsigned long long>(s));
   }
-  const uint64_t s = wave_sum_u64(start ? 1u : 0u);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(n_pairs, static_cast<unsigned long long>(s));
 }
 
 __global__ void k_fill_u16(uint16_t* a, uint64_t n, uint16_t v) {
-  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (i < n) a[i] = v;
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t i = blk_ * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = v;
+  }
 }
 
 // pieces of each task (piece starts: the task's first edge and every pair start)
@@ -1038,18 +1067,20 @@ __global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, uint3
                              const uint64_t* gstart, const uint32_t* gtask, const uint32_t* bits32,
                              const uint32_t* task_piece, uint32_t* piece_row,
                              uint32_t* piece_stream) {
-  const uint64_t e = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (e >= n) return;
-  const uint64_t k = key[e];
-  const uint32_t gr = group_of_key(G, k);
-  const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + (e - gstart[gr]);
-  bool st = false;
-  const uint32_t pc = piece_of(bits32, task_piece, pos, &st);
-  if (st) {
-    piece_row[pc] = static_cast<uint32_t>(k >> G.qb) & ((1u << G.rb) - 1u);
-    const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
-    const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
-    piece_stream[pc] = sl * nseg + seg;
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    if (e >= n) continue;
+    const uint64_t k = key[e];
+    const uint32_t gr = group_of_key(G, k);
+    const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + (e - gstart[gr]);
+    bool st = false;
+    const uint32_t pc = piece_of(bits32, task_piece, pos, &st);
+    if (st) {
+      piece_row[pc] = static_cast<uint32_t>(k >> G.qb) & ((1u << G.rb) - 1u);
+      const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
+      const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
+      piece_stream[pc] = sl * nseg + seg;
+    }
   }
 }
 
@@ -1067,23 +1098,29 @@ __device__ __forceinline__ uint32_t block_row0(const RowBlocks& B, uint32_t b) {
 // per-piece row offset in its block + run starts T[block][stream] (sentinel where empty)
 __global__ void k_runs(const uint32_t* prow, const uint32_t* pstream, uint64_t np, RowBlocks B,
                        uint16_t* roff, uint32_t* T, uint32_t* sstart) {
-  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (i >= np) return;
-  const uint32_t l = prow[i], k = pstream[i], b = block_of_row(B, l);
-  roff[i] = static_cast<uint16_t>(l - block_row0(B, b));
-  const bool first = i == 0 || pstream[i - 1] != k || block_of_row(B, prow[i - 1]) != b;
-  if (first) T[static_cast<uint64_t>(b) * B.NS + k] = static_cast<uint32_t>(i);
-  if (i == 0 || pstream[i - 1] != k) sstart[k] = static_cast<uint32_t>(i);
+  PRMI_BLOCK_LOOP(np) {
+    const uint64_t i = blk_ * blockDim.x + threadIdx.x;
+    if (i >= np) continue;
+    const uint32_t l = prow[i], k = pstream[i], b = block_of_row(B, l);
+    roff[i] = static_cast<uint16_t>(l - block_row0(B, b));
+    const bool first = i == 0 || pstream[i - 1] != k || block_of_row(B, prow[i - 1]) != b;
+    if (first) T[static_cast<uint64_t>(b) * B.NS + k] = static_cast<uint32_t>(i);
+    if (i == 0 || pstream[i - 1] != k) sstart[k] = static_cast<uint32_t>(i);
+  }
 }
 
 __global__ void k_fill_f64(double* a, uint64_t n, double v) {
-  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (i < n) a[i] = v;
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t i = blk_ * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = v;
+  }
 }
 
 __global__ void k_iota(uint32_t* a, uint64_t n) {
-  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (i < n) a[i] = static_cast<uint32_t>(i);
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t i = blk_ * blockDim.x + threadIdx.x;
+    if (i < n) a[i] = static_cast<uint32_t>(i);
+  }
 }
 
 __global__ void k_local_meta(const uint32_t* perm, const uint32_t* outdeg, const uint32_t* dang_w,
@@ -1097,41 +1134,47 @@ __global__ void k_local_meta(const uint32_t* perm, const uint32_t* outdeg, const
 // export: (internal row << 32 | internal source) of every stream edge
 __global__ void k_piece_row_runs(const uint32_t* T, const uint16_t* roff, RowBlocks B,
                                  uint32_t* piece_row) {
-  const uint64_t t = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (t >= static_cast<uint64_t>(B.NB) * B.NS) return;
-  const uint32_t b = static_cast<uint32_t>(t / B.NS);
-  const uint32_t r0 = block_row0(B, b);
-  for (uint32_t i = T[t]; i < T[t + B.NS]; ++i) piece_row[i] = r0 + roff[i];
+  PRMI_BLOCK_LOOP(static_cast<uint64_t>(B.NB) * B.NS) {
+    const uint64_t t = blk_ * blockDim.x + threadIdx.x;
+    if (t >= static_cast<uint64_t>(B.NB) * B.NS) continue;
+    const uint32_t b = static_cast<uint32_t>(t / B.NS);
+    const uint32_t r0 = block_row0(B, b);
+    for (uint32_t i = T[t]; i < T[t + B.NS]; ++i) piece_row[i] = r0 + roff[i];
+  }
 }
 __global__ void k_export_keys(const uint32_t* col, const uint16_t* col16, const uint32_t* bits32,
                               const uint32_t* task_piece, const uint32_t* piece_row, Layout L,
                               const uint64_t* gstart, const uint32_t* gtask, const uint64_t* gbase,
                               uint32_t ngroups, uint32_t nlds, uint32_t H, uint64_t stream_len,
                               uint64_t* out) {
-  const uint64_t pos = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (pos >= stream_len) return;
-  const uint32_t t = static_cast<uint32_t>(pos / TASK);
-  uint32_t lo = 0, hi = ngroups - 1;  // last group whose first task <= t
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1) / 2;
-    if (gtask[mid] <= t) lo = mid; else hi = mid - 1;
+  PRMI_BLOCK_LOOP(stream_len) {
+    const uint64_t pos = blk_ * blockDim.x + threadIdx.x;
+    if (pos >= stream_len) continue;
+    const uint32_t t = static_cast<uint32_t>(pos / TASK);
+    uint32_t lo = 0, hi = ngroups - 1;  // last group whose first task <= t
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) / 2;
+      if (gtask[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t rel = pos - static_cast<uint64_t>(gtask[lo]) * TASK;
+    if (rel >= gstart[lo + 1] - gstart[lo]) continue;  // padding
+    const uint32_t pc = piece_of(bits32, task_piece, pos, nullptr);
+    const uint32_t row = row_of(L, piece_row[pc]);
+    const uint32_t j = lo / (nlds + 1), gi = lo % (nlds + 1);
+    uint32_t xp;
+    if (gi < nlds) xp = (j % L.p) * L.maxA + (j / L.p) * L.SL + gi * H + col16[gbase[lo] + rel];
+    else xp = col[gbase[lo] + rel];
+    out[gstart[lo] + rel] = (static_cast<uint64_t>(row) << 32) | col_of_xpos(L, xp);
   }
-  const uint64_t rel = pos - static_cast<uint64_t>(gtask[lo]) * TASK;
-  if (rel >= gstart[lo + 1] - gstart[lo]) return;  // padding
-  const uint32_t pc = piece_of(bits32, task_piece, pos, nullptr);
-  const uint32_t row = row_of(L, piece_row[pc]);
-  const uint32_t j = lo / (nlds + 1), gi = lo % (nlds + 1);
-  uint32_t xp;
-  if (gi < nlds) xp = (j % L.p) * L.maxA + (j / L.p) * L.SL + gi * H + col16[gbase[lo] + rel];
-  else xp = col[gbase[lo] + rel];
-  out[gstart[lo] + rel] = (static_cast<uint64_t>(row) << 32) | col_of_xpos(L, xp);
 }
 __global__ void k_export_split(const uint64_t* key, uint64_t n, uint32_t* col, uint64_t* row_ptr) {
-  const uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t k = key[i];
-  col[i] = static_cast<uint32_t>(k);
-  if (i == 0 || (key[i - 1] >> 32) != (k >> 32)) row_ptr[k >> 32] = i;
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t i = blk_ * blockDim.x + threadIdx.x;
+    if (i >= n) continue;
+    const uint64_t k = key[i];
+    col[i] = static_cast<uint32_t>(k);
+    if (i == 0 || (key[i - 1] >> 32) != (k >> 32)) row_ptr[k >> 32] = i;
+  }
 }
 
 __global__ void k_scatter_ranks(const uint32_t* perm, const double* r_loc, uint32_t lrows,
@@ -1150,7 +1193,12 @@ __global__ void k_sources_one(const uint32_t* outdeg, uint32_t n, double* r_full
 // =======================================================================================
 namespace {
 
+// blocks for n items, capped: kernels over edge-sized ranges loop (PRMI_BLOCK_LOOP) past it;
+// the others are launched on vertex counts (< 2^32 / BLOCK blocks)
 inline uint32_t grid_for(uint64_t n) { return static_cast<uint32_t>((n + BLOCK - 1) / BLOCK); }
+inline uint32_t grid_loop(uint64_t n) {
+  return static_cast<uint32_t>(std::min<uint64_t>((n + BLOCK - 1) / BLOCK, 1u << 22));
+}
 
 int bits_for(uint64_t n) {
   if (n <= 2) return 1;
@@ -1263,14 +1311,14 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     }
   } guard{&kA, &kB};
   if (in.rmat) {
-    if (m) hipLaunchKernelGGL(k_rmat_keys, dim3(grid_for(m)), dim3(BLOCK), 0, s, in.seed, in.scale, m, kA);
+    if (m) hipLaunchKernelGGL(k_rmat_keys, dim3(grid_loop(m)), dim3(BLOCK), 0, s, in.seed, in.scale, m, kA);
   } else if (m) {
     uint32_t *ds = nullptr, *dd = nullptr;
     TRY(dmalloc(&ds, m, err));
     TRY(dmalloc(&dd, m, err));
     HIPTRY(hipMemcpyAsync(ds, in.h_src, m * 4, hipMemcpyHostToDevice, s));
     HIPTRY(hipMemcpyAsync(dd, in.h_dst, m * 4, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_make_keys, dim3(grid_for(m)), dim3(BLOCK), 0, s, ds, dd, m, nb, kA);
+    hipLaunchKernelGGL(k_make_keys, dim3(grid_loop(m)), dim3(BLOCK), 0, s, ds, dd, m, nb, kA);
     HIPTRY(hipStreamSynchronize(s));
     (void)hipFree(ds);
     (void)hipFree(dd);
@@ -1311,7 +1359,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   HIPTRY(hipMemsetAsync(d_sums, 0, 32, s));
   HIPTRY(hipMemsetAsync(g->outdeg, 0, 4ull * (n ? n : 1), s));
   HIPTRY(hipMemsetAsync(g->indeg, 0, 4ull * (n ? n : 1), s));
-  if (nnz) hipLaunchKernelGGL(k_degrees, dim3(grid_for(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, g->outdeg, g->indeg, d_sums);
+  if (nnz) hipLaunchKernelGGL(k_degrees, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, g->outdeg, g->indeg, d_sums);
   uint32_t* d_mapw = nullptr;
   if (in.h_mapw) {
     TRY(dmalloc(&d_mapw, n, err));
@@ -1437,7 +1485,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&d_cnt, 2 + NG, err));
   HIPTRY(hipMemsetAsync(d_cnt, 0, 16, s));
   HIPTRY(hipMemsetAsync(d_cnt + 2, 0xFF, 8ull * NG, s));
-  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_for(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, d_cnt, lk_in);
+  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, d_cnt, lk_in);
   uint64_t lnnz = nnz;
   if (p > 1) {
     HIPTRY(hipMemcpyAsync(&lnnz, d_cnt, 8, hipMemcpyDeviceToHost, s));
@@ -1453,7 +1501,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     if (lnnz) HIPTRY(rocprim::radix_sort_keys(tmp.p, tb, db, lnnz, 0, key_bits, s));
     lk = db.current();
   }
-  if (lnnz) hipLaunchKernelGGL(k_group_starts, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, d_cnt + 2);
+  if (lnnz) hipLaunchKernelGGL(k_group_starts, dim3(grid_loop(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, d_cnt + 2);
   std::vector<unsigned long long> hst(NG);
   HIPTRY(hipMemcpyAsync(hst.data(), d_cnt + 2, 8ull * NG, hipMemcpyDeviceToHost, s));
   HIPTRY(hipStreamSynchronize(s));
@@ -1496,10 +1544,10 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&g->col16, g->n_col16, err));
   TRY(dmalloc(&g->bits, g->stream_len / EPL + 2, err));
   HIPTRY(hipMemsetAsync(g->col, 0xFF, 4 * std::max<uint64_t>(g->n_col32, 1), s));  // PAD_COL
-  if (g->n_col16) hipLaunchKernelGGL(k_fill_u16, dim3(grid_for(g->n_col16)), dim3(BLOCK), 0, s, g->col16, g->n_col16, static_cast<uint16_t>(G.H));  // zero slot
+  if (g->n_col16) hipLaunchKernelGGL(k_fill_u16, dim3(grid_loop(g->n_col16)), dim3(BLOCK), 0, s, g->col16, g->n_col16, static_cast<uint16_t>(G.H));  // zero slot
   HIPTRY(hipMemsetAsync(g->bits, 0, 2 * (g->stream_len / EPL + 2), s));
   uint32_t* bits32 = reinterpret_cast<uint32_t*>(g->bits);
-  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, g->d_gstart, g->d_gtask, g->d_gbase, g->col, g->col16, bits32, d_cnt + 1);
+  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_loop(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, g->d_gstart, g->d_gtask, g->d_gbase, g->col, g->col16, bits32, d_cnt + 1);
   TRY(dmalloc(&g->task_piece, tasks + 1ull, err));
   {
     uint32_t* tcnt = nullptr;
@@ -1542,8 +1590,8 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     TRY(dmalloc(&g->runs, tn, err));
     HIPTRY(hipMemsetAsync(g->runs, 0xFF, 4 * tn, s));
     HIPTRY(hipMemsetAsync(sst, 0xFF, 4ull * RBk.NS, s));
-    if (lnnz) hipLaunchKernelGGL(k_piece_rows, dim3(grid_for(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, g->nseg, g->d_gstart, g->d_gtask, bits32, g->task_piece, prow, pstream);
-    if (NP) hipLaunchKernelGGL(k_runs, dim3(grid_for(NP)), dim3(BLOCK), 0, s, prow, pstream, NP, RBk, g->roff, g->runs, sst);
+    if (lnnz) hipLaunchKernelGGL(k_piece_rows, dim3(grid_loop(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, g->nseg, g->d_gstart, g->d_gtask, bits32, g->task_piece, prow, pstream);
+    if (NP) hipLaunchKernelGGL(k_runs, dim3(grid_loop(NP)), dim3(BLOCK), 0, s, prow, pstream, NP, RBk, g->roff, g->runs, sst);
     // fill the empty runs: T[NB][k] = end of stream k, T[b][k] = T[b+1][k] where empty
     std::vector<uint32_t> hT(tn), hs(RBk.NS);
     HIPTRY(hipMemcpyAsync(hT.data(), g->runs, 4 * tn, hipMemcpyDeviceToHost, s));
@@ -1577,7 +1625,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   (void)hipFree(vid);
   TRY(dmalloc(&g->partial, NP, err));
   // PR_DBG experiments may skip the partial stores: keep every rank defined
-  if (T.dbg && NP) hipLaunchKernelGGL(k_fill_f64, dim3(grid_for(NP)), dim3(BLOCK), 0, s, g->partial, NP, 1.0);
+  if (T.dbg && NP) hipLaunchKernelGGL(k_fill_f64, dim3(grid_loop(NP)), dim3(BLOCK), 0, s, g->partial, NP, 1.0);
 
   // ---- iteration buffers ----------------------------------------------------------------
   TRY(dmalloc(&g->r_loc[0], lrows, err));
@@ -1672,9 +1720,15 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   if (g->ntask) launch_stream(g, S, s);
   if (g->nb_rows) {
     const dim3 gr(g->nb_rows), bl(BLOCK);
-    if (mode == 0) hipLaunchKernelGGL(spmv_rows<0>, gr, bl, 0, s, A);
-    else if (mode == 1) hipLaunchKernelGGL(spmv_rows<1>, gr, bl, 0, s, A);
-    else hipLaunchKernelGGL(spmv_rows<2>, gr, bl, 0, s, A);
+    if (A.NS <= 512) {
+      if (mode == 0) hipLaunchKernelGGL((spmv_rows<0, 512>), gr, bl, 0, s, A);
+      else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1, 512>), gr, bl, 0, s, A);
+      else hipLaunchKernelGGL((spmv_rows<2, 512>), gr, bl, 0, s, A);
+    } else {
+      if (mode == 0) hipLaunchKernelGGL((spmv_rows<0, MAX_NS>), gr, bl, 0, s, A);
+      else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1, MAX_NS>), gr, bl, 0, s, A);
+      else hipLaunchKernelGGL((spmv_rows<2, MAX_NS>), gr, bl, 0, s, A);
+    }
   }
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
   hipLaunchKernelGGL(reduce_shards, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local);
@@ -1723,15 +1777,15 @@ int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s,
   TRY(dmalloc(&rp, g->lrows + 1ull, err)); fr.v.push_back(rp);
   TRY(dmalloc(&c, m, err)); fr.v.push_back(c);
   const RowBlocks RBk{g->lA, g->nb_rows_a, g->nb_rows, g->n_streams};
-  if (g->nb_rows) hipLaunchKernelGGL(k_piece_row_runs, dim3(grid_for(static_cast<uint64_t>(g->nb_rows) * g->n_streams)), dim3(BLOCK), 0, s, g->runs, g->roff, RBk, prow);
-  if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_for(g->stream_len)), dim3(BLOCK), 0, s, g->col, g->col16, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, g->d_gstart, g->d_gtask, g->d_gbase, static_cast<uint32_t>(g->gtask.size() - 1), g->nlds, g->hot_h, g->stream_len, k0);
+  if (g->nb_rows) hipLaunchKernelGGL(k_piece_row_runs, dim3(grid_loop(static_cast<uint64_t>(g->nb_rows) * g->n_streams)), dim3(BLOCK), 0, s, g->runs, g->roff, RBk, prow);
+  if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_loop(g->stream_len)), dim3(BLOCK), 0, s, g->col, g->col16, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, g->d_gstart, g->d_gtask, g->d_gbase, static_cast<uint32_t>(g->gtask.size() - 1), g->nlds, g->hot_h, g->stream_len, k0);
   rocprim::double_buffer<uint64_t> db(k0, k1);
   size_t tb = 0;
   HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, m, 0, 64, s));
   TRY(tmp.ensure(tb, err));
   if (m) HIPTRY(rocprim::radix_sort_keys(tmp.p, tb, db, m, 0, 64, s));
   HIPTRY(hipMemsetAsync(rp, 0, 8ull * (g->lrows + 1), s));
-  if (m) hipLaunchKernelGGL(k_export_split, dim3(grid_for(m)), dim3(BLOCK), 0, s, db.current(), m, c, rp);
+  if (m) hipLaunchKernelGGL(k_export_split, dim3(grid_loop(m)), dim3(BLOCK), 0, s, db.current(), m, c, rp);
   HIPTRY(hipGetLastError());
   if (row_ptr) HIPTRY(hipMemcpyAsync(row_ptr, rp, 8ull * g->lrows, hipMemcpyDeviceToHost, s));
   if (col && m) HIPTRY(hipMemcpyAsync(col, c, 4ull * m, hipMemcpyDeviceToHost, s));
