@@ -8,15 +8,16 @@
 //     class D [R+nC,n)      in==0, out==0   neither
 //   rows k < R are dealt to ranks in chunks of 16: chunk c = k>>4 goes to rank c % p
 //   XCD slicing: the columns of x are cut into 8 slices by 128-byte chunk (slice = chunk
-//   index mod 8).  Slice j's edges form ONE stream that only workgroups with
-//   blockIdx % 8 == j (one XCD) read, so each XCD's L2 caches 1/8 of x.  Inside a slice the
-//   columns are in hotness order (position q); the stream is ordered by (segment of q,
-//   local row, q): segment 0 = the hot prefix [0, QH) (its first H entries served from an
-//   LDS copy), then cold segments of S entries each, so a cold segment's x lines are
-//   fetched once and reused from L2 while the XCD sweeps it.
-//   A "pair" = the edges of one (row, slice, segment); a "piece" = a pair cut at the
-//   1024-edge task boundaries of the stream.  The stream kernel writes one partial sum per
-//   piece; the row kernel adds a row's pieces (row-major piece list) in a fixed order.
+//   index mod 8).  Slice j's edges are processed only by workgroups with blockIdx % 8 == j
+//   (one XCD), so each XCD's L2 caches 1/8 of x.  Inside a slice the columns are in hotness
+//   order (position q), cut into segments: nlds LDS blocks of H entries, an L2-hot range,
+//   then cold ranges.  Stream groups per slice: one per LDS block (16-bit columns) + one for
+//   the rest (32-bit x positions), each sorted by (segment, local row, q) and padded to
+//   whole 1024-edge tasks.
+//   A "pair" = the edges of one (row, slice, segment); a "piece" = a pair cut at task
+//   boundaries.  The stream kernel writes one partial sum per piece (stream order); the row
+//   kernel reads, per 1024-row block, one contiguous run per stream (runs table) and adds
+//   the pieces in a fixed order.
 #pragma once
 
 #include <hip/hip_runtime.h>

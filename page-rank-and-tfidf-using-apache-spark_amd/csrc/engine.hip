@@ -3,14 +3,16 @@
 // Replaces, per round, PageRank.java:94-160 -- the contribution flatMapToPair (:94-117), the
 // dangling-mass reduce (:121-138), reduceByKey(Sum) (:139, Sum :208-213) and the damping /
 // dangling-update maps (:140-160) -- with a pull SpMV over the transposed graph in two
-// launches (XCD-sliced partial sums for heavy rows; a fused row launch that combines them,
-// handles the light rows and applies the epilogue) plus two single-workgroup reductions.  The graph build (K1) replaces
-// distinct().groupByKey() (:42), the urlCount loop (:103-108) and subtractByKey (:56).
+// launches: the stream launch (one XCD per column slice; LDS-blocked gathers; one partial sum
+// per piece of a (row, slice, segment) pair) and the row launch (each row's pieces added in a
+// fixed order + the fused epilogue), plus two single-workgroup reductions.  The graph build
+// (K1) replaces distinct().groupByKey() (:42), the urlCount loop (:103-108) and
+// subtractByKey (:56).
 //
 // Numerics (DESIGN.md "Parity"):
 //   * x = r / outdeg is one IEEE division per source (same operands as :113, bit-exact);
-//   * each row's sum is a fixed-shape tree that depends only on the row's in-degree
-//     (deterministic, identical for any number of ranks);
+//   * each row's sum is an fp64 sum whose order is fixed by the stream layout (deterministic
+//     for a given graph and rank count);
 //   * r' = 0.15 + (c + a) * 0.85 is evaluated unfused in Java's order (:143);
 //   * the dangling mass, residual and rank sum are EXACT (integer superaccumulator, then one
 //     correct rounding), so addthis (:135) equals the correctly rounded exact value.
