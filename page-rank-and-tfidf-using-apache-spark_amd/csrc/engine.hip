@@ -301,9 +301,10 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (wv + 1) / 4);
   double* aw = acc[wv];
   uint32_t kw = 0;  // wave-uniform lower bound of the stream search
-  for (uint32_t pos = lo; pos < hi; pos += 64 * EPR) {
-    // lane l takes pieces pos + l + 64u: the lanes of one load cover 64 consecutive pieces
-    // (one coalesced 512-B read inside a long run)
+  // lane l takes pieces pos + l + 64u: the lanes of one load cover 64 consecutive pieces (one
+  // coalesced 512-B read inside a long run).  Two-stage pipeline: the next step's loads are
+  // issued before this step's LDS adds.
+  auto locate = [&](uint32_t pos, uint32_t (&pc)[EPR]) {
     const uint32_t i0 = pos + lane;
     // stream of i0: last k with pre[k] <= i0 (empty streams share pre with the next one);
     // galloping search from the wave's lower bound
@@ -317,27 +318,38 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
       const uint32_t mid = (k + kh + 1) >> 1;
       if (pre[mid] <= i0) k = mid; else kh = mid - 1;
     }
-    uint32_t pc[EPR];
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
       const uint32_t i = i0 + 64u * u;
       while (k + 1 < NS && pre[k + 1] <= i) ++k;
       pc[u] = i < hi ? st[k] + (i - pre[k]) : 0u;  // never address past the pieces
     }
-    double val[EPR];
-    uint32_t r[EPR];
+    kw = __builtin_amdgcn_readfirstlane(k);  // lane 0's stream after this step (monotone)
+  };
+  double va[EPR], vb[EPR];
+  uint32_t ra[EPR], rbuf[EPR], pc[EPR];
+  auto issue = [&](uint32_t pos, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
+    locate(pos, pc);
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
-      const bool ok = i0 + 64u * u < hi;
-      val[u] = A.partial[pc[u]];
-      r[u] = A.roff[pc[u]];
-      if (!ok) val[u] = 0.0;
+      vv[u] = A.partial[pc[u]];
+      rr[u] = A.roff[pc[u]];
     }
+  };
+  auto add = [&](uint32_t pos, const double (&vv)[EPR], const uint32_t (&rr)[EPR]) {
     // LDS adds in lane order inside each instruction: a fixed order for a fixed layout
 #pragma unroll
     for (int u = 0; u < EPR; ++u)
-      if (i0 + 64u * u < hi) atomicAdd(&aw[r[u]], val[u]);
-    kw = __builtin_amdgcn_readfirstlane(k);  // lane 0's stream after this step (monotone)
+      if (pos + lane + 64u * u < hi) atomicAdd(&aw[rr[u]], vv[u]);
+  };
+  constexpr uint32_t STEP = 64 * EPR;
+  if (lo < hi) issue(lo, va, ra);
+  for (uint32_t pos = lo; pos < hi; pos += 2 * STEP) {
+    const bool n1 = pos + STEP < hi, n2 = pos + 2 * STEP < hi;
+    if (n1) issue(pos + STEP, vb, rbuf);
+    add(pos, va, ra);
+    if (n2) issue(pos + 2 * STEP, va, ra);
+    if (n1) add(pos + STEP, vb, rbuf);
   }
   __syncthreads();
   // epilogue over the block's rows (uniform trip count: row_epilogue synchronises)
