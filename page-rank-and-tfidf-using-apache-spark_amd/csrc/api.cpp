@@ -188,46 +188,158 @@ PairIndex make_pair_index(const pr_ctx* c) {
 
 // PageRank.java:167-189: ranks.join(mappings) -> (rank,(id,title)) -> sortByKey(false) ->
 // take(k).  Ties (unspecified order in Spark) broken by (title bytes, id).
-int topk_rows(pr_ctx* c, uint32_t k, std::vector<uint64_t>* pairs_out) {
-  int rc = gather_ranks(c);
+struct TopRow {
+  double r;
+  uint64_t pair;
+  uint32_t v;
+};
+
+// Candidates of the whole job: every rank selects on its device (dev_topk_candidates) over
+// its own pages; the union holds the global top k (ranks own disjoint pages).
+int topk_candidates(pr_ctx* c, uint64_t k, std::vector<uint32_t>* ids, std::vector<double>* rs) {
+  if (c->last_iters < 0) return fail(c, PR_E_ARG, "no completed pr_run");
+  int rc = need_device(c);
+  if (rc) return rc;
+  ids->clear();
+  rs->clear();
+  std::vector<uint32_t> mi;
+  std::vector<double> mr;
+  std::string err;
+  if (!c->group.empty()) {
+    for (pr_ctx* m : c->group) {
+      HIPCHK(c, hipSetDevice(m->device));
+      rc = prmi::dev_scatter_ranks(&m->dg, c->last_iters, m->stream);
+      if (!rc) rc = prmi::dev_topk_candidates(&m->dg, k, &mi, &mr, m->stream, &err);
+      if (rc) {
+        (void)hipSetDevice(c->device);
+        return fail(c, rc, "top-K selection: " + err);
+      }
+      ids->insert(ids->end(), mi.begin(), mi.end());
+      rs->insert(rs->end(), mr.begin(), mr.end());
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    return PR_OK;
+  }
+  rc = prmi::dev_scatter_ranks(&c->dg, c->last_iters, c->stream);
+  if (!rc) rc = prmi::dev_topk_candidates(&c->dg, k, ids, rs, c->stream, &err);
+  if (rc) return fail(c, rc, "top-K selection: " + err);
+  const int p = c->opts.n_ranks;
+  if (p <= 1) return PR_OK;
+  // all-gather the per-rank candidate counts, then the candidates padded to the largest count
+  uint64_t* d_cnt = nullptr;
+  HIPCHK(c, hipMalloc(&d_cnt, 8ull * p));
+  std::vector<uint64_t> cnt(p);
+  cnt[c->opts.rank] = ids->size();
+  HIPCHK(c, hipMemcpyAsync(d_cnt + c->opts.rank, &cnt[c->opts.rank], 8, hipMemcpyHostToDevice, c->stream));
+  ncclResult_t nr = ncclAllGather(d_cnt + c->opts.rank, d_cnt, 1, ncclUint64, c->comm, c->stream);
+  if (nr == ncclSuccess) {
+    (void)hipMemcpyAsync(cnt.data(), d_cnt, 8ull * p, hipMemcpyDeviceToHost, c->stream);
+    (void)hipStreamSynchronize(c->stream);
+  }
+  (void)hipFree(d_cnt);
+  if (nr != ncclSuccess) return fail(c, PR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+  const uint64_t M = *std::max_element(cnt.begin(), cnt.end());
+  if (M == 0) return PR_OK;
+  uint32_t* d_ids = nullptr;
+  double* d_rs = nullptr;
+  HIPCHK(c, hipMalloc(&d_ids, 4ull * M * p));
+  if (hipMalloc(&d_rs, 8ull * M * p) != hipSuccess) {
+    (void)hipFree(d_ids);
+    return fail(c, PR_E_OOM, "top-K exchange buffers");
+  }
+  const uint64_t off = static_cast<uint64_t>(c->opts.rank) * M;
+  std::vector<uint32_t> ai(M * p);
+  std::vector<double> ar(M * p);
+  bool ok = true;
+  if (!ids->empty()) {
+    ok = ok && hipMemcpyAsync(d_ids + off, ids->data(), 4 * ids->size(), hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    ok = ok && hipMemcpyAsync(d_rs + off, rs->data(), 8 * rs->size(), hipMemcpyHostToDevice, c->stream) == hipSuccess;
+  }
+  nr = ncclGroupStart();
+  if (nr == ncclSuccess) nr = ncclAllGather(d_ids + off, d_ids, M, ncclUint32, c->comm, c->stream);
+  if (nr == ncclSuccess) nr = ncclAllGather(d_rs + off, d_rs, M, ncclFloat64, c->comm, c->stream);
+  const ncclResult_t ge = ncclGroupEnd();
+  if (nr == ncclSuccess) nr = ge;
+  if (nr == ncclSuccess) {
+    ok = ok && hipMemcpyAsync(ai.data(), d_ids, 4ull * M * p, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
+    ok = ok && hipMemcpyAsync(ar.data(), d_rs, 8ull * M * p, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
+  }
+  ok = hipStreamSynchronize(c->stream) == hipSuccess && ok;
+  (void)hipFree(d_ids);
+  (void)hipFree(d_rs);
+  if (nr != ncclSuccess) return fail(c, PR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+  if (!ok) return fail(c, PR_E_HIP, "top-K exchange copies");
+  ids->clear();
+  rs->clear();
+  for (int q = 0; q < p; ++q)
+    for (uint64_t i = 0; i < cnt[q]; ++i) {
+      ids->push_back(ai[q * M + i]);
+      rs->push_back(ar[q * M + i]);
+    }
+  return PR_OK;
+}
+
+// text graphs: the mapping pairs of every id (pairs grouped by id, in pair order)
+void ensure_pairs_by_id(pr_ctx* c) {
+  HostGraph& h = c->hg;
+  if (h.pair_first.size() == static_cast<size_t>(h.n) + 1) return;
+  h.pair_first.assign(static_cast<size_t>(h.n) + 1, 0);
+  for (uint32_t id : h.pair_id) h.pair_first[id + 1]++;
+  for (uint32_t v = 0; v < h.n; ++v) h.pair_first[v + 1] += h.pair_first[v];
+  h.pairs_by_id.resize(h.pair_id.size());
+  std::vector<uint64_t> at(h.pair_first.begin(), h.pair_first.end() - 1);
+  for (uint64_t i = 0; i < h.pair_id.size(); ++i) h.pairs_by_id[at[h.pair_id[i]]++] = i;
+}
+
+int topk_rows(pr_ctx* c, uint32_t k, std::vector<TopRow>* out) {
+  out->clear();
+  std::vector<uint32_t> ids;
+  std::vector<double> rs;
+  int rc = topk_candidates(c, k, &ids, &rs);
   if (rc) return rc;
   const PairIndex pi = make_pair_index(c);
-  const uint64_t np = pair_count(c);
-  struct Row {
-    double r;
-    uint64_t pair;
-    uint32_t v;
-  };
-  std::vector<Row> rows;
-  rows.reserve(std::min<uint64_t>(np, 1u << 20));
-  for (uint64_t i = 0; i < np; ++i) {
-    uint32_t v;
-    if (c->source == pr_ctx::SRC_TEXT) v = c->hg.pair_id[i];
-    else if (c->hg.mapw.empty()) v = static_cast<uint32_t>(i);
-    else {
-      std::string t;
-      pair_at(c, pi, i, &v, &t);
+  if (c->source == pr_ctx::SRC_TEXT) ensure_pairs_by_id(c);
+  std::vector<TopRow> rows;
+  for (size_t i = 0; i < ids.size(); ++i) {
+    const uint32_t v = ids[i];
+    uint64_t b = v, e = v + 1ull;  // the pairs of page v
+    if (c->source == pr_ctx::SRC_TEXT) {
+      b = c->hg.pair_first[v];
+      e = c->hg.pair_first[v + 1];
+    } else if (!c->hg.mapw.empty()) {
+      b = pi.first[v];
+      e = pi.first[v + 1];
     }
-    const double r = c->h_ranks[v];
-    if (r > 0.0) rows.push_back({r, i, v});
+    for (uint64_t q = b; q < e; ++q)
+      rows.push_back({rs[i], c->source == pr_ctx::SRC_TEXT ? c->hg.pairs_by_id[q] : q, v});
   }
-  std::vector<std::string> tcache;
-  auto title_of = [&](const Row& x) {
-    uint32_t v;
-    std::string t;
-    pair_at(c, pi, x.pair, &v, &t);
-    return t;
-  };
-  auto less = [&](const Row& a, const Row& b) {
-    if (a.r != b.r) return a.r > b.r;
-    const std::string ta = title_of(a), tb = title_of(b);
-    if (ta != tb) return ta < tb;
-    return a.v < b.v;
-  };
+  // rank descending; runs of equal rank (ties) then by (title bytes, page), titles built
+  // only for the tied runs that reach into the first k rows
+  std::sort(rows.begin(), rows.end(), [](const TopRow& a, const TopRow& b) {
+    return a.r != b.r ? a.r > b.r : a.pair < b.pair;
+  });
   const size_t kk = std::min<size_t>(k, rows.size());
-  std::partial_sort(rows.begin(), rows.begin() + kk, rows.end(), less);
-  pairs_out->clear();
-  for (size_t i = 0; i < kk; ++i) pairs_out->push_back(rows[i].pair);
+  std::vector<std::pair<std::string, TopRow>> run;
+  for (size_t a = 0; a < kk;) {
+    size_t b = a + 1;
+    while (b < rows.size() && rows[b].r == rows[a].r) ++b;
+    if (b - a > 1) {
+      run.clear();
+      for (size_t q = a; q < b; ++q) {
+        uint32_t vv;
+        std::string t;
+        pair_at(c, pi, rows[q].pair, &vv, &t);
+        run.emplace_back(std::move(t), rows[q]);
+      }
+      std::sort(run.begin(), run.end(), [](const auto& x, const auto& y) {
+        return x.first != y.first ? x.first < y.first : x.second.v < y.second.v;
+      });
+      for (size_t q = a; q < b; ++q) rows[q] = run[q - a].second;
+    }
+    a = b;
+  }
+  rows.resize(kk);
+  *out = std::move(rows);
   return PR_OK;
 }
 
@@ -656,17 +768,13 @@ int pr_get_ranks(pr_ctx* c, double* out, uint64_t n) {
 int pr_topk(pr_ctx* c, uint32_t k, uint64_t* pair_out, uint32_t* id_out, double* rank_out,
             uint32_t* count) {
   if (!c) return PR_E_ARG;
-  std::vector<uint64_t> rows;
+  std::vector<TopRow> rows;
   int rc = topk_rows(c, k, &rows);
   if (rc) return rc;
-  const PairIndex pi = make_pair_index(c);
   for (size_t i = 0; i < rows.size(); ++i) {
-    uint32_t v;
-    std::string t;
-    pair_at(c, pi, rows[i], &v, &t);
-    if (pair_out) pair_out[i] = rows[i];
-    if (id_out) id_out[i] = v;
-    if (rank_out) rank_out[i] = c->h_ranks[v];
+    if (pair_out) pair_out[i] = rows[i].pair;
+    if (id_out) id_out[i] = rows[i].v;
+    if (rank_out) rank_out[i] = rows[i].r;
   }
   if (count) *count = static_cast<uint32_t>(rows.size());
   return PR_OK;
@@ -674,18 +782,18 @@ int pr_topk(pr_ctx* c, uint32_t k, uint64_t* pair_out, uint32_t* id_out, double*
 
 int pr_write_top_page(pr_ctx* c, const char* path) {
   if (!c) return PR_E_ARG;
-  std::vector<uint64_t> rows;
+  std::vector<TopRow> rows;
   int rc = topk_rows(c, c->opts.topk, &rows);
   if (rc) return rc;
   if (c->opts.rank != 0) return PR_OK;
   const PairIndex pi = make_pair_index(c);
   std::string out;
   char num[64];
-  for (uint64_t i : rows) {
+  for (const TopRow& row : rows) {
     uint32_t v;
     std::string t;
-    pair_at(c, pi, i, &v, &t);
-    prmi::java_double_to_string(c->h_ranks[v], num, sizeof(num));
+    pair_at(c, pi, row.pair, &v, &t);
+    prmi::java_double_to_string(row.r, num, sizeof(num));
     out += t;
     out += '\t';
     out += num;

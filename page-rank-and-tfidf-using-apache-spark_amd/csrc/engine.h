@@ -106,6 +106,7 @@ struct DevGraph {
   uint32_t* outdeg = nullptr;     // by original id
   uint32_t* indeg = nullptr;
   uint32_t* dang_w = nullptr;
+  uint32_t* mapw = nullptr;       // [n] mapping pairs per page (nullptr: every page once)
   double* x_init = nullptr;
   double* xbuf[2] = {nullptr, nullptr};
   double* r_loc[2] = {nullptr, nullptr};
@@ -151,6 +152,11 @@ double* dev_x_out(DevGraph* g, int t);
 // iterations == 0 reproduces ranks = 1.0 on sources (PageRank.java:76-83).
 int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s);
 // Host copy of this rank's pull CSR (single-rank graphs: internal ids, sources ascending).
+// Top-K candidates of this rank (PageRank.java:167-189): every mapped page whose rank is >=
+// the k-th largest rank counted with mapping-pair multiplicity among this rank's pages
+// (ties at the boundary included), from r_full (call dev_scatter_ranks first).
+int dev_topk_candidates(DevGraph* g, uint64_t k, std::vector<uint32_t>* ids,
+                        std::vector<double>* rs, hipStream_t s, std::string* err);
 int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s, std::string* err);
 // Internal id of this rank's local row l (host copy of the device mapping).
 inline uint32_t row_internal(const DevGraph* g, uint32_t l) {

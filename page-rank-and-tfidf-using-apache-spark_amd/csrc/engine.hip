@@ -1202,6 +1202,51 @@ __global__ void k_sources_one(const uint32_t* outdeg, uint32_t n, double* r_full
   if (v < n) r_full[v] = outdeg[v] ? 1.0 : 0.0;
 }
 
+// ---- top-K selection (PageRank.java:167-189 join(mappings) + sortByKey(false) + take(k)) --
+// A weighted radix select over the bit patterns of r_full: defined ranks are positive
+// doubles, which order like their bits.  A page weighs its number of mapping pairs (the
+// join at :167 emits one record per (id, title); ids outside the mapping weigh 0 and never
+// reach the output).  Digits of SEL_BITS from the top; pass d histograms, per digit, the
+// weight and the page count of the pages whose key matches the prefix chosen so far.
+constexpr int SEL_BITS = 11, SEL_BINS = 1 << SEL_BITS;
+__global__ __launch_bounds__(BLOCK) void k_select_hist(const double* r, const uint32_t* mapw,
+                                                       uint32_t n, uint64_t prefix, uint64_t pmask,
+                                                       int shift, uint32_t dmask,
+                                                       unsigned long long* hist) {
+  __shared__ unsigned long long hw[SEL_BINS], hc[SEL_BINS];
+  for (int i = threadIdx.x; i < SEL_BINS; i += BLOCK) hw[i] = hc[i] = 0;
+  __syncthreads();
+  for (uint32_t v = blockIdx.x * BLOCK + threadIdx.x; v < n; v += gridDim.x * BLOCK) {
+    const uint64_t key = static_cast<uint64_t>(__double_as_longlong(r[v]));
+    const uint32_t w = mapw ? mapw[v] : 1u;
+    if (key == 0 || w == 0 || (key & pmask) != prefix) continue;
+    const uint32_t d = static_cast<uint32_t>(key >> shift) & dmask;
+    atomicAdd(&hw[d], static_cast<unsigned long long>(w));
+    atomicAdd(&hc[d], 1ull);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i <= static_cast<int>(dmask); i += BLOCK)
+    if (hc[i]) {
+      atomicAdd(&hist[i], hw[i]);
+      atomicAdd(&hist[SEL_BINS + i], hc[i]);
+    }
+}
+
+// every mapped page whose key is >= lb (order of the output is arbitrary; the host sorts)
+__global__ void k_select_emit(const double* r, const uint32_t* mapw, uint32_t n, uint64_t lb,
+                              uint32_t* ids, double* rs, unsigned* cnt, uint32_t cap) {
+  const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
+  if (v >= n) return;
+  const double x = r[v];
+  const uint64_t key = static_cast<uint64_t>(__double_as_longlong(x));
+  if (key < lb || (mapw && mapw[v] == 0)) return;
+  const unsigned i = atomicAdd(cnt, 1u);
+  if (i < cap) {
+    ids[i] = v;
+    rs[i] = x;
+  }
+}
+
 // =======================================================================================
 // host side of the build
 // =======================================================================================
@@ -1261,7 +1306,7 @@ void dev_free(DevGraph* g) {
   F(g->d_gtask); F(g->d_gstart); F(g->d_gbase); F(g->col16);
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
-  F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state);
+  F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->mapw);
   const int p = g->p, rank = g->rank;
   *g = DevGraph();
   g->p = p;
@@ -1405,7 +1450,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   (void)hipFree(d_sums);
   (void)hipFree(vk);
   (void)hipFree(vk2);
-  if (d_mapw) (void)hipFree(d_mapw);
+  g->mapw = d_mapw;  // kept: the top-K selection weighs pages by their mapping pairs
   g->digest[0] = sums[0];
   g->digest[1] = sums[1];
   g->W0 = sums[2];
@@ -1770,6 +1815,81 @@ int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s) {
     hipLaunchKernelGGL(k_scatter_ranks, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->perm, g->r_loc[iterations & 1], g->lrows, layout_of(g), g->r_full);
   }
   HIPTRY(hipGetLastError());
+  return PR_OK;
+}
+
+int dev_topk_candidates(DevGraph* g, uint64_t k, std::vector<uint32_t>* ids,
+                        std::vector<double>* rs, hipStream_t s, std::string* err) {
+  ids->clear();
+  rs->clear();
+  const uint32_t n = g->n;
+  if (k == 0 || n == 0) return PR_OK;
+  constexpr uint64_t CAP = 1u << 16;  // stop refining once the boundary digit holds <= CAP
+  unsigned long long* hist = nullptr;
+  TRY(dmalloc(&hist, 2 * SEL_BINS, err));
+  struct Free {
+    std::vector<void*> v;
+    ~Free() { for (void* p : v) if (p) (void)hipFree(p); }
+  } fr;
+  fr.v.push_back(hist);
+  std::vector<unsigned long long> h(2 * SEL_BINS);
+  uint64_t prefix = 0, pmask = 0, need = k, count = 0;  // count: pages with key >= lb
+  int top = 64;
+  const uint32_t grid = std::min<uint32_t>(grid_for(n), 4096);
+  while (top > 0) {
+    const int shift = std::max(top - SEL_BITS, 0), width = top - shift;
+    const uint32_t dmask = (1u << width) - 1;
+    HIPTRY(hipMemsetAsync(hist, 0, 16ull * SEL_BINS, s));
+    hipLaunchKernelGGL(k_select_hist, dim3(grid), dim3(BLOCK), 0, s, g->r_full, g->mapw, n,
+                       prefix, pmask, shift, dmask, hist);
+    HIPTRY(hipGetLastError());
+    HIPTRY(hipMemcpyAsync(h.data(), hist, 16ull * SEL_BINS, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    uint64_t above = 0;
+    int d = static_cast<int>(dmask);
+    for (; d >= 0; --d) {
+      if (above + h[d] >= need) break;
+      above += h[d];
+      count += h[SEL_BINS + d];
+    }
+    if (d < 0) break;  // (first pass only) fewer than k weighted pages: take them all
+    need -= above;
+    prefix |= static_cast<uint64_t>(d) << shift;
+    pmask |= static_cast<uint64_t>(dmask) << shift;
+    top = shift;
+    if (h[d] <= CAP || top == 0) {
+      count += h[SEL_BINS + d];
+      break;
+    }
+  }
+  const uint64_t lb = std::max<uint64_t>(prefix, 1);
+  if (count == 0) return PR_OK;
+  if (count > 0xFFFFFFFFull) {
+    if (err) *err = "top-K candidate set too large";
+    return PR_E_ARG;
+  }
+  uint32_t* d_ids = nullptr;
+  double* d_rs = nullptr;
+  unsigned* d_cnt = nullptr;
+  TRY(dmalloc(&d_ids, count, err)); fr.v.push_back(d_ids);
+  TRY(dmalloc(&d_rs, count, err)); fr.v.push_back(d_rs);
+  TRY(dmalloc(&d_cnt, 1, err)); fr.v.push_back(d_cnt);
+  HIPTRY(hipMemsetAsync(d_cnt, 0, 4, s));
+  hipLaunchKernelGGL(k_select_emit, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->r_full, g->mapw, n,
+                     lb, d_ids, d_rs, d_cnt, static_cast<uint32_t>(count));
+  HIPTRY(hipGetLastError());
+  unsigned got = 0;
+  HIPTRY(hipMemcpyAsync(&got, d_cnt, 4, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipStreamSynchronize(s));
+  if (got != count) {
+    if (err) *err = "top-K selection: candidate count mismatch";
+    return PR_E_HIP;
+  }
+  ids->resize(count);
+  rs->resize(count);
+  HIPTRY(hipMemcpyAsync(ids->data(), d_ids, 4ull * count, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(rs->data(), d_rs, 8ull * count, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipStreamSynchronize(s));
   return PR_OK;
 }
 

@@ -41,6 +41,8 @@ struct HostGraph {
   std::vector<uint32_t> pair_len;
   std::string titles;
   uint64_t n_pairs = 0;           // == pair_id.size() for text graphs; == sum(mapw) otherwise
+  // pairs grouped by id (built on the first top-K of a text graph)
+  std::vector<uint64_t> pair_first, pairs_by_id;
 };
 
 struct ParseError {
