@@ -549,7 +549,20 @@ int pr_ingest_buffers(pr_ctx* c, const char* arcs, size_t alen, const char* map,
   c->hg = HostGraph();
   c->have_graph = false;
   prmi::ParseError pe;
-  if (!prmi::ingest_text(arcs ? arcs : "", alen, map ? map : "", mlen, &c->hg, &pe)) {
+  bool parsed = true;
+  if (c->has_device) {  // device ingest (ingest.hip); host parser for host-only contexts
+    std::string err;
+    HIPCHK(c, hipSetDevice(c->device));
+    rc = prmi::dev_ingest_text(arcs ? arcs : "", alen, map ? map : "", mlen, &c->hg, &pe, c->stream, &err);
+    if (rc == PR_E_PARSE) parsed = false;
+    else if (rc) {
+      c->hg = HostGraph();
+      return fail(c, rc, "device ingest: " + err);
+    }
+  } else {
+    parsed = prmi::ingest_text(arcs ? arcs : "", alen, map ? map : "", mlen, &c->hg, &pe);
+  }
+  if (!parsed) {
     c->hg = HostGraph();
     return fail(c, PR_E_PARSE,
                 std::string("java.lang.ArrayIndexOutOfBoundsException: 1 (") +

@@ -26,6 +26,8 @@
 #include <string>
 #include <vector>
 
+#include "host_graph.h"
+
 namespace prmi {
 
 constexpr int SA_LIMBS = 10;       // exact accumulator: 10 x 32-bit chunks, unit 2^-96
@@ -157,6 +159,10 @@ int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s);
 // (ties at the boundary included), from r_full (call dev_scatter_ranks first).
 int dev_topk_candidates(DevGraph* g, uint64_t k, std::vector<uint32_t>* ids,
                         std::vector<double>* rs, hipStream_t s, std::string* err);
+// Text ingest on the device (ingest.hip): same result as ingest_text (host_graph.cpp).
+// PR_E_PARSE with *pe filled on a malformed line.
+int dev_ingest_text(const char* arcs, size_t alen, const char* map, size_t mlen, HostGraph* g,
+                    ParseError* pe, hipStream_t s, std::string* err);
 int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s, std::string* err);
 // Internal id of this rank's local row l (host copy of the device mapping).
 inline uint32_t row_internal(const DevGraph* g, uint32_t l) {

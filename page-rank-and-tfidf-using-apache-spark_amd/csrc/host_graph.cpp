@@ -41,24 +41,7 @@ static inline uint64_t hash_bytes(const char* p, size_t n) {
 
 StrTable::StrTable() : slots_(1024, 0) {}
 
-void StrTable::reserve(size_t entries, size_t bytes) {
-  off_.reserve(entries);
-  len_.reserve(entries);
-  arena_.reserve(bytes);
-  size_t cap = slots_.size();
-  while (cap < entries * 2) cap *= 2;
-  if (cap != slots_.size()) {
-    slots_.assign(cap, 0);
-    for (uint64_t i = 0; i < off_.size(); ++i) {
-      uint64_t h = hash_bytes(arena_.data() + off_[i], len_[i]) & (cap - 1);
-      while (slots_[h]) h = (h + 1) & (cap - 1);
-      slots_[h] = i + 1;
-    }
-  }
-}
-
-void StrTable::grow() {
-  size_t cap = slots_.size() * 2;
+void StrTable::rehash(size_t cap) {
   std::vector<uint64_t> ns(cap, 0);
   for (uint64_t i = 0; i < off_.size(); ++i) {
     uint64_t h = hash_bytes(arena_.data() + off_[i], len_[i]) & (cap - 1);
@@ -66,9 +49,34 @@ void StrTable::grow() {
     ns[h] = i + 1;
   }
   slots_.swap(ns);
+  indexed_ = true;
+}
+
+void StrTable::reserve(size_t entries, size_t bytes) {
+  off_.reserve(entries);
+  len_.reserve(entries);
+  arena_.reserve(bytes);
+  size_t cap = slots_.size();
+  while (cap < entries * 2) cap *= 2;
+  if (cap != slots_.size() || !indexed_) rehash(cap);
+}
+
+void StrTable::grow() { rehash(slots_.size() * 2); }
+
+void StrTable::adopt(std::string arena, std::vector<uint64_t> off, std::vector<uint32_t> len) {
+  arena_ = std::move(arena);
+  off_ = std::move(off);
+  len_ = std::move(len);
+  slots_.assign(1024, 0);
+  indexed_ = false;
 }
 
 uint32_t StrTable::intern(const char* p, size_t n, bool* is_new) {
+  if (!indexed_) {
+    size_t cap = 1024;
+    while (cap < (off_.size() + 1) * 2) cap *= 2;
+    rehash(cap);
+  }
   if ((off_.size() + 1) * 2 > slots_.size()) grow();
   const uint64_t mask = slots_.size() - 1;
   uint64_t h = hash_bytes(p, n) & mask;

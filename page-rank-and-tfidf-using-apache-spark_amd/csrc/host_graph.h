@@ -18,9 +18,14 @@ class StrTable {
     return arena_.data() + off_[i];
   }
   void reserve(size_t entries, size_t bytes);
+  // take over strings already distinct and in index order (the device ingest); the hash
+  // index is rebuilt on the next intern()
+  void adopt(std::string arena, std::vector<uint64_t> off, std::vector<uint32_t> len);
 
  private:
   void grow();
+  void rehash(size_t cap);
+  bool indexed_ = true;
   std::vector<uint64_t> slots_;  // 0 empty, else index + 1
   std::vector<uint64_t> off_;
   std::vector<uint32_t> len_;

@@ -112,3 +112,38 @@ def rmat_text(scale: int, edge_factor: int, seed: int) -> Tuple[bytes, bytes]:
     arcs = "".join(f"{a}\t{b}\n" for a, b in zip(s.tolist(), d.tolist())).encode()
     maps = "".join(f"{i}\tv{i}\n" for i in range(1 << scale)).encode()
     return arcs, maps
+
+
+def big_text(seed: int, pages: int, arcs: int) -> Tuple[bytes, bytes]:
+    """Large fixed-width wiki-style input built with numpy (ingest scale tests / timing):
+    7-digit ids, Zipf-skewed destinations, one title per page plus a second title on 1% of
+    pages, ~2% duplicate arc lines, ~1% arcs to ids outside the mapping."""
+    rng = np.random.default_rng(seed)
+    ids = rng.permutation(9_000_000)[:pages + pages // 50] + 1_000_000
+    mapped, unmapped = ids[:pages], ids[pages:]
+
+    def digits(v):
+        out = np.empty((len(v), 7), np.uint8)
+        x = v.copy()
+        for c in range(6, -1, -1):
+            out[:, c] = 48 + x % 10
+            x //= 10
+        return out
+
+    src = mapped[rng.integers(0, pages, arcs)]
+    dst = mapped[np.minimum(rng.zipf(1.3, arcs) - 1, pages - 1)]
+    stray = rng.random(arcs) < 0.01
+    dst[stray] = unmapped[rng.integers(0, len(unmapped), int(stray.sum()))]
+    dup = rng.random(arcs) < 0.02
+    src[1:][dup[1:]] = src[:-1][dup[1:]]
+    dst[1:][dup[1:]] = dst[:-1][dup[1:]]
+    a = np.empty((arcs, 16), np.uint8)
+    a[:, 0:7], a[:, 7], a[:, 8:15], a[:, 15] = digits(src), 9, digits(dst), 10
+    m1 = np.empty((pages, 22), np.uint8)      # "ddddddd\tPage ddddddd\n"
+    m1[:, 0:7], m1[:, 7], m1[:, 8:13], m1[:, 13:20] = digits(mapped), 9, list(b"Page "), digits(mapped)
+    m1[:, 20], m1[:, 21] = ord("x"), 10
+    two = mapped[rng.random(pages) < 0.01]
+    m2 = np.empty((len(two), 22), np.uint8)
+    m2[:, 0:7], m2[:, 7], m2[:, 8:13], m2[:, 13:20] = digits(two), 9, list(b"Alt  "), digits(two)
+    m2[:, 20], m2[:, 21] = ord("y"), 10
+    return a.tobytes(), m1.tobytes() + m2.tobytes()
