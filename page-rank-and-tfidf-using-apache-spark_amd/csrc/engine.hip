@@ -182,6 +182,7 @@ struct RowArgs {
   const IterState* st;
   uint64_t* shards;
   uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
+  uint32_t dbg;              // PR_DBG timing experiments: 16 no LDS adds, 32 no epilogue, 64 no pieces
 };
 
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
@@ -199,31 +200,26 @@ __device__ __forceinline__ T ld_stream(const T* p) {
   else return *p;
 }
 
-// Epilogue for one row per group leader, then the block's exact partials (dangling mass +
-// count for class-B rows; residual + rank sum in tracked mode) into the atomic shards.
+// Epilogue of one row (leader = the row exists): r', x' or the row's dangling weight, and in
+// tracked mode r'; the exact partials (dangling mass + count for class-B rows; residual +
+// rank sum in tracked mode) go into this wave's LDS record (flushed once per block).
 template <int MODE>
-__device__ __forceinline__ void row_epilogue(const RowArgs& A, double a, uint32_t cls,
-                                             uint32_t row, double c, bool leader,
-                                             uint64_t (*lds)[REC_WORDS]) {
+__device__ __forceinline__ void row_finish(const RowArgs& A, double a, uint32_t cls,
+                                           uint32_t row, double c, bool leader, uint32_t mt,
+                                           double ro, uint64_t* lw) {
   double r = 0.0;
   uint32_t w = 0;
   if (leader) {
     // PageRank.java:143  0.15 + (sum + addthis) * 0.85, unfused
     r = c > 0.0 ? __dadd_rn(0.15, __dmul_rn(__dadd_rn(c, a), 0.85)) : 0.0;
-    const uint32_t mt = A.meta[row];
     if (cls == 0)
       A.x_out[xslot_of(A, row)] = r / static_cast<double>(mt);  // :113  rank / urlCount
     else
       w = mt;
     if (MODE >= 1) A.r_out[row] = r;
   }
-  const bool acc = (cls == 1) || (MODE == 2);  // uniform over the workgroup
-  if (!acc) return;
-  for (int i = threadIdx.x; i < 4 * REC_WORDS; i += BLOCK) (&lds[0][0])[i] = 0;
-  __syncthreads();
-  uint64_t* lw = lds[threadIdx.x >> 6];
   uint32_t c0, c1, c2, c3;
-  if (cls == 1) {
+  if (cls == 1) {  // uniform over the workgroup
     // PageRank.java:125-134  sum of danglingMap values (w entries per page)
     const int li = sa_chunks(leader ? r : 0.0, w, c0, c1, c2, c3);
     wave_accum_sa(lw, REC_DSUM, li, c0, c1, c2, c3);
@@ -231,15 +227,16 @@ __device__ __forceinline__ void row_epilogue(const RowArgs& A, double a, uint32_
     if ((threadIdx.x & 63) == 0) lw[REC_DCNT] += cnt;
   }
   if (MODE == 2) {
-    double ro = 0.0;
-    if (leader) ro = A.r_old ? A.r_old[row] : 1.0;
     const double d = fabs(r - ro);
     int li = sa_chunks(leader ? d : 0.0, 1u, c0, c1, c2, c3);
     wave_accum_sa(lw, REC_RESID, li, c0, c1, c2, c3);
     li = sa_chunks(leader ? r : 0.0, 1u, c0, c1, c2, c3);
     wave_accum_sa(lw, REC_RSUM, li, c0, c1, c2, c3);
   }
-  __syncthreads();
+}
+
+// the block's 4 wave records -> one atomic shard (after a barrier)
+__device__ __forceinline__ void flush_records(const RowArgs& A, uint64_t (*lds)[REC_WORDS]) {
   if (threadIdx.x < REC_WORDS) {
     const int t = threadIdx.x;
     const uint64_t s = (lds[0][t] + lds[1][t]) + (lds[2][t] + lds[3][t]);
@@ -261,6 +258,21 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   const uint32_t b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < 4 * RB; i += BLOCK) (&acc[0][0])[i] = 0.0;
+  for (int i = tid; i < 4 * REC_WORDS; i += BLOCK) (&lds[0][0])[i] = 0;
+  // the block's rows; their epilogue inputs are loaded now, used after the piece loop
+  const bool clsB = b >= A.nbA;
+  const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * RB : b * RB;
+  const uint32_t rb1 = min(rb0 + RB, clsB ? A.lrows : A.lA);
+  constexpr int RPT = RB / BLOCK;  // rows per thread
+  uint32_t mt[RPT];
+  double ro[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const uint32_t row = rb0 + tid + q * BLOCK;
+    mt[q] = row < rb1 ? A.meta[row] : 0u;
+    ro[q] = 0.0;
+    if (MODE == 2 && row < rb1) ro[q] = A.r_old ? A.r_old[row] : 1.0;
+  }
   // run lengths of the block's streams -> exclusive prefix pre[] (SPT streams per thread)
   const uint32_t NS = A.NS;
   const uint32_t* T0 = A.T + static_cast<uint64_t>(b) * NS;
@@ -326,7 +338,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     }
     kw = __builtin_amdgcn_readfirstlane(k);  // lane 0's stream after this step (monotone)
   };
-  double va[EPR], vb[EPR];
+  double va[EPR], vb[EPR], sink = 0.0;
   uint32_t ra[EPR], rbuf[EPR], pc[EPR];
   auto issue = [&](uint32_t pos, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
     locate(pos, pc);
@@ -340,28 +352,38 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     // LDS adds in lane order inside each instruction: a fixed order for a fixed layout
 #pragma unroll
     for (int u = 0; u < EPR; ++u)
-      if (pos + lane + 64u * u < hi) atomicAdd(&aw[rr[u]], vv[u]);
+      if (pos + lane + 64u * u < hi) {
+        if (A.dbg & 16u) sink += vv[u] + rr[u];
+        else atomicAdd(&aw[rr[u]], vv[u]);
+      }
   };
   constexpr uint32_t STEP = 64 * EPR;
-  if (lo < hi) issue(lo, va, ra);
-  for (uint32_t pos = lo; pos < hi; pos += 2 * STEP) {
+  const uint32_t hi_loop = (A.dbg & 64u) ? lo : hi;  // timing: no piece loads at all
+  if (lo < hi_loop) issue(lo, va, ra);
+  for (uint32_t pos = lo; pos < hi_loop; pos += 2 * STEP) {
     const bool n1 = pos + STEP < hi, n2 = pos + 2 * STEP < hi;
     if (n1) issue(pos + STEP, vb, rbuf);
     add(pos, va, ra);
     if (n2) issue(pos + 2 * STEP, va, ra);
     if (n1) add(pos + STEP, vb, rbuf);
   }
+  if (A.dbg & 16u) aw[lane] = sink;
   __syncthreads();
-  // epilogue over the block's rows (uniform trip count: row_epilogue synchronises)
-  const bool clsB = b >= A.nbA;
-  const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * RB : b * RB;
-  const uint32_t rb1 = min(rb0 + RB, clsB ? A.lrows : A.lA);
+  if (A.dbg & 32u) return;
+  // epilogue over the block's rows
   const double a = A.st->a;
-  for (int l = tid; l < RB; l += BLOCK) {
+  uint64_t* lw = lds[wv];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int l = tid + q * BLOCK;
     const uint32_t row = rb0 + l;
-    const bool active = row < rb1;
-    const double c = (acc[0][l] + acc[1][l]) + (acc[2][l] + acc[3][l]);
-    row_epilogue<MODE>(A, a, clsB ? 1u : 0u, row, c, active, lds);
+    double c = (acc[0][l] + acc[1][l]) + (acc[2][l] + acc[3][l]);
+    if (A.dbg & 64u) c = 1.0;
+    row_finish<MODE>(A, a, clsB ? 1u : 0u, row, c, row < rb1, mt[q], ro[q], lw);
+  }
+  if (clsB || MODE == 2) {  // uniform over the workgroup
+    __syncthreads();
+    flush_records(A, lds);
   }
 }
 
@@ -1761,6 +1783,7 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.T = g->runs;
   A.partial = g->partial;
   A.roff = g->roff;
+  A.dbg = static_cast<uint32_t>(g->tune.dbg);
   A.NS = g->n_streams;
   A.nbA = g->nb_rows_a;
   A.lA = g->lA;
