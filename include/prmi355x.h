@@ -65,6 +65,10 @@ typedef struct {
 
 #define PR_F_TRACK_RESIDUAL 0x1u /* compute the exact L1 residual every iteration          */
 #define PR_F_VERBOSE 0x2u        /* phase timings on stderr                                */
+#define PR_F_NORMALIZED 0x4u     /* normalized PageRank (not in the reference):
+                                    r^0 = 1/N_tot and r' = 0.15/N_tot + (c + a)*0.85, so the
+                                    ranks sum to ~1 instead of ~N_tot (PageRank.java:78,:143
+                                    use 1.0 and 0.15)                                       */
 
 typedef struct {
   int32_t iterations;     /* iterations executed                                          */
@@ -145,6 +149,20 @@ int pr_graph_get_info(pr_ctx* ctx, pr_graph_info* out);
  * (implies PR_F_TRACK_RESIDUAL).  Returns PR_E_EMPTY_DANGLING where the reference job
  * would die at :125 (stats->failed_iteration says which round).  Collective. */
 int pr_run(pr_ctx* ctx, int32_t iterations, double tol, pr_stats* stats);
+
+/* Resume (the reference has no checkpoint).  pr_set_ranks seeds the
+ * following pr_run calls with ranks by vertex id (as pr_get_ranks returns them, 0.0 =
+ * undefined) reached after `rounds_done` >= 1 rounds: pr_run(T) then computes rounds
+ * rounds_done+1 .. rounds_done+T of one uninterrupted run, bit-identical to it (the seed's
+ * x = r/outdeg and exact dangling mass equal the engine's own).  Only pages with in-links
+ * may carry a rank.  ranks == NULL clears the seed.  Every rank passes the whole vector.
+ * pr_checkpoint_save writes the last run's ranks with the total round count and the graph's
+ * identity (vertex count, nnz, N_tot, edge digest, PR_F_NORMALIZED); rank 0 writes, the
+ * call is collective.  pr_checkpoint_load checks the identity against the current graph
+ * and seeds from the file. */
+int pr_set_ranks(pr_ctx* ctx, const double* ranks, uint64_t n, int32_t rounds_done);
+int pr_checkpoint_save(pr_ctx* ctx, const char* path);
+int pr_checkpoint_load(pr_ctx* ctx, const char* path);
 
 /* Final `ranks` RDD as a dense array indexed by vertex id (0.0 = no rank: the page is
  * absent from the reference's ranks RDD).  n must be >= n_vertices.  Collective. */

@@ -67,6 +67,9 @@ def lib():
                                        C.POINTER(D), C.POINTER(I32), C.POINTER(D)]
         L.orc_run.restype = I32
         L.orc_run.argtypes = [P, I32, I32, I32, D, P, C.POINTER(D), C.POINTER(I32), C.POINTER(D)]
+        L.orc_run_ex.restype = I32
+        L.orc_run_ex.argtypes = [P, I32, I32, I32, D, I32, P, P, C.POINTER(D), C.POINTER(I32),
+                                 C.POINTER(D)]
         L.orc_exact_dot_u32.restype = D
         L.orc_exact_dot_u32.argtypes = [P, P, U64]
         L.orc_free.restype = None
@@ -75,8 +78,8 @@ def lib():
     return _lib
 
 
-def _ptr(a: np.ndarray):
-    return a.ctypes.data_as(C.c_void_p)
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
 class OracleError(Exception):
@@ -175,12 +178,18 @@ class Graph:
 
     # ---- the job ----
     def run(self, iterations: int = 10, exact: bool = True, threads: int = 0,
-            tol: float = 0.0) -> Dict[str, object]:
+            tol: float = 0.0, normalized: bool = False, r_init=None) -> Dict[str, object]:
+        """normalized: r^0 = 1/N_tot and base 0.15/N_tot; r_init: resume from these ranks."""
         self.check()
         r = np.zeros(self.n, np.float64)
         spi, done, resid = C.c_double(0), C.c_int(0), C.c_double(0)
-        rc = lib().orc_run(self._h, iterations, int(exact), threads, tol, _ptr(r), C.byref(spi),
-                           C.byref(done), C.byref(resid))
+        if normalized or r_init is not None:
+            ri = None if r_init is None else np.ascontiguousarray(r_init, np.float64)
+            rc = lib().orc_run_ex(self._h, iterations, int(exact), threads, tol, int(normalized),
+                                  _ptr(ri), _ptr(r), C.byref(spi), C.byref(done), C.byref(resid))
+        else:
+            rc = lib().orc_run(self._h, iterations, int(exact), threads, tol, _ptr(r),
+                               C.byref(spi), C.byref(done), C.byref(resid))
         if rc:
             raise OracleError(rc, done.value)
         return {"ranks": r, "sec_per_iter": spi.value, "iterations": done.value,

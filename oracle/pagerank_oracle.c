@@ -420,16 +420,19 @@ static double now_s(void) { struct timespec t; clock_gettime(CLOCK_MONOTONIC, &t
  * exact=1: exact sums; exact=0: plain fp64 (baseline).  tol>0: stop once
  * sum|r'-r| / sum r' <= tol (r^0 = 1 everywhere).  Returns 0 or ORC_E_EMPTY_DANGLING;
  * *iters_done = iterations performed (the failing one included on error). */
-int orc_pagerank_csr(uint32_t n, const uint64_t* row_ptr, const uint32_t* col,
-                     const uint32_t* outdeg, const uint32_t* dang_w, uint64_t n_tot,
-                     int iterations, int exact, int threads, double tol,
-                     double* ranks_out, double* sec_per_iter, int* iters_done,
-                     double* last_resid) {
+/* The general form: r0 = initial rank of every page, base = damping base (1.0 and 0.15 for
+ * PageRank.java:78,:143; 1/N_tot and 0.15/N_tot for the normalized option); r_init != NULL
+ * starts from those ranks instead (a resumed run). */
+int orc_pagerank_csr_ex(uint32_t n, const uint64_t* row_ptr, const uint32_t* col,
+                        const uint32_t* outdeg, const uint32_t* dang_w, uint64_t n_tot,
+                        int iterations, int exact, int threads, double tol, double r0,
+                        double base, const double* r_init, double* ranks_out,
+                        double* sec_per_iter, int* iters_done, double* last_resid) {
   if (threads > 0) omp_set_num_threads(threads);
   double* r = ranks_out;
   double* x = malloc(8 * (size_t)(n ? n : 1));
   double* rn = malloc(8 * (size_t)(n ? n : 1));
-  for (uint32_t v = 0; v < n; ++v) r[v] = 1.0;
+  for (uint32_t v = 0; v < n; ++v) r[v] = r_init ? r_init[v] : r0;
   int rc = ORC_OK, t = 0;
   double t0 = now_s(), resid = -1.0;
   for (t = 1; t <= iterations; ++t) {
@@ -458,14 +461,14 @@ int orc_pagerank_csr(uint32_t n, const uint64_t* row_ptr, const uint32_t* col,
         superacc acc; sa_zero(&acc);
         for (uint64_t e = row_ptr[d]; e < row_ptr[d + 1]; ++e) sa_add(&acc, x[col[e]]);
         double c = sa_to_double(&acc);
-        rn[d] = c > 0.0 ? 0.15 + (c + addthis) * 0.85 : 0.0;
+        rn[d] = c > 0.0 ? base + (c + addthis) * 0.85 : 0.0;
       }
     } else {
 #pragma omp parallel for schedule(dynamic, 1024)
       for (int64_t d = 0; d < (int64_t)n; ++d) {
         double c = 0.0;
         for (uint64_t e = row_ptr[d]; e < row_ptr[d + 1]; ++e) c += x[col[e]];
-        rn[d] = c > 0.0 ? 0.15 + (c + addthis) * 0.85 : 0.0;
+        rn[d] = c > 0.0 ? base + (c + addthis) * 0.85 : 0.0;
       }
     }
     if (tol > 0.0) {
@@ -482,10 +485,20 @@ int orc_pagerank_csr(uint32_t n, const uint64_t* row_ptr, const uint32_t* col,
   if (iters_done) *iters_done = done;
   if (sec_per_iter) *sec_per_iter = done > 0 ? el / done : 0.0;
   if (last_resid) *last_resid = resid;
-  if (iterations == 0)       /* the loop never ran: ranks = sources at 1.0 (:76-83) */
-    for (uint32_t v = 0; v < n; ++v) r[v] = outdeg[v] ? 1.0 : 0.0;
+  if (iterations == 0 && !r_init) /* the loop never ran: ranks = sources at r0 (:76-83) */
+    for (uint32_t v = 0; v < n; ++v) r[v] = outdeg[v] ? r0 : 0.0;
   free(x); free(rn);
   return rc;
+}
+
+int orc_pagerank_csr(uint32_t n, const uint64_t* row_ptr, const uint32_t* col,
+                     const uint32_t* outdeg, const uint32_t* dang_w, uint64_t n_tot,
+                     int iterations, int exact, int threads, double tol,
+                     double* ranks_out, double* sec_per_iter, int* iters_done,
+                     double* last_resid) {
+  return orc_pagerank_csr_ex(n, row_ptr, col, outdeg, dang_w, n_tot, iterations, exact, threads,
+                             tol, 1.0, 0.15, NULL, ranks_out, sec_per_iter, iters_done,
+                             last_resid);
 }
 
 int orc_run(const orc_graph* g, int iterations, int exact, int threads, double tol,
@@ -493,6 +506,18 @@ int orc_run(const orc_graph* g, int iterations, int exact, int threads, double t
   if (g->err) return g->err;
   return orc_pagerank_csr(g->n, g->row_ptr, g->col, g->outdeg, g->dang_w, g->n_tot, iterations,
                           exact, threads, tol, ranks_out, sec_per_iter, iters_done, last_resid);
+}
+
+/* normalized: r0 = 1/N_tot, base = 0.15/N_tot; r_init: resume from those ranks */
+int orc_run_ex(const orc_graph* g, int iterations, int exact, int threads, double tol,
+               int normalized, const double* r_init, double* ranks_out, double* sec_per_iter,
+               int* iters_done, double* last_resid) {
+  if (g->err) return g->err;
+  const double r0 = normalized ? 1.0 / (double)g->n_tot : 1.0;
+  const double base = normalized ? 0.15 / (double)g->n_tot : 0.15;
+  return orc_pagerank_csr_ex(g->n, g->row_ptr, g->col, g->outdeg, g->dang_w, g->n_tot,
+                             iterations, exact, threads, tol, r0, base, r_init, ranks_out,
+                             sec_per_iter, iters_done, last_resid);
 }
 
 /* exact-sum helper exported for tests: correctly rounded sum of w[i]*v[i] */

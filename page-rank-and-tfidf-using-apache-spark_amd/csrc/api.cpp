@@ -11,6 +11,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cmath>
+#include <cstdint>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -41,6 +43,7 @@ struct pr_ctx {
   std::vector<double> h_ranks;
   double ms_ingest = 0;
   std::vector<pr_ctx*> group;    // single-process rank group (pr_comm_init_local)
+  int seed_rounds = 0;           // pr_set_ranks: rounds behind the seed (0 = no seed)
 };
 
 namespace {
@@ -83,8 +86,11 @@ int need_comm(pr_ctx* c) {
   return PR_OK;
 }
 
-int build_device(pr_ctx* c, const prmi::BuildInput& in) {
+int build_device(pr_ctx* c, const prmi::BuildInput& in0) {
   std::string e;
+  prmi::BuildInput in = in0;
+  in.normalized = (c->opts.flags & PR_F_NORMALIZED) != 0;
+  c->seed_rounds = 0;
   int rc = prmi::dev_build(&c->dg, in, c->stream, &e);
   if (rc) return fail(c, rc, "device build: " + e);
   c->last_iters = -1;
@@ -697,7 +703,8 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
     if (st) *st = s;
     return PR_OK;
   }
-  if (g->W0 == 0) {  // round 1 reduces an empty danglingMap (PageRank.java:125)
+  const int t0 = g->seeded ? c->seed_rounds : 0;  // rounds behind the starting ranks
+  if (!g->seeded && g->W0 == 0) {  // round 1 reduces an empty danglingMap (PageRank.java:125)
     s.failed_iteration = 1;
     if (st) *st = s;
     return fail(c, PR_E_EMPTY_DANGLING, "java.lang.UnsupportedOperationException: empty collection (iteration 1)");
@@ -758,11 +765,11 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   s.rank_sum = tracked ? hs.rank_sum : 0.0;
   // the reduce of round err_iter saw an empty danglingMap: the reference dies there
   if (hs.err_iter != 0 && hs.err_iter <= done) {
-    s.failed_iteration = hs.err_iter;
+    s.failed_iteration = t0 + hs.err_iter;
     if (st) *st = s;
     return fail(c, PR_E_EMPTY_DANGLING,
                 "java.lang.UnsupportedOperationException: empty collection (iteration " +
-                    std::to_string(hs.err_iter) + ")");
+                    std::to_string(t0 + hs.err_iter) + ")");
   }
   c->last_iters = done;
   if (st) *st = s;
@@ -918,3 +925,105 @@ int pr_format_double(double v, char* buf, size_t cap) {
 }
 
 }  // extern "C"
+
+// ---- resume / checkpoint ----------------------------------------------
+namespace {
+
+struct CkptHeader {
+  char magic[8];        // "PRMICKP1"
+  uint32_t version;     // 1
+  uint32_t flags;       // PR_F_NORMALIZED of the run
+  uint64_t n, nnz, n_tot, digest0, digest1;
+  int64_t rounds;       // rounds behind the ranks
+};
+static_assert(sizeof(CkptHeader) == 64, "checkpoint header layout");
+
+int seed_one(pr_ctx* c, const double* ranks, uint64_t n, int32_t rounds_done) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  std::string err;
+  if (!ranks) {
+    c->last_iters = -1;
+    c->host_ranks_valid = false;
+    c->seed_rounds = 0;
+    rc = prmi::dev_seed_state(&c->dg, nullptr, c->stream, &err);
+    return rc ? fail(c, rc, "seed: " + err) : PR_OK;
+  }
+  if (n != c->dg.n) return fail(c, PR_E_ARG, "ranks: length != vertex count");
+  if (rounds_done < 1) return fail(c, PR_E_ARG, "rounds_done must be >= 1 (round 0 is r^0: start fresh instead)");
+  std::vector<uint32_t> indeg(n);
+  if (n) HIPCHK(c, hipMemcpyAsync(indeg.data(), c->dg.indeg, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint64_t v = 0; v < n; ++v) {
+    const double r = ranks[v];
+    if (!(r >= 0.0) || r == HUGE_VAL)
+      return fail(c, PR_E_ARG, "ranks: page " + std::to_string(v) + " is negative or not finite");
+    if (r > 0.0 && indeg[v] == 0)
+      return fail(c, PR_E_ARG, "ranks: page " + std::to_string(v) + " has no in-link, so no rank after round 1");
+  }
+  c->last_iters = -1;  // the seed replaces the last run's state
+  c->host_ranks_valid = false;
+  rc = prmi::dev_seed_state(&c->dg, ranks, c->stream, &err);
+  if (rc) return fail(c, rc, "seed: " + err);
+  c->seed_rounds = rounds_done;
+  return PR_OK;
+}
+
+}  // namespace
+
+int pr_set_ranks(pr_ctx* c, const double* ranks, uint64_t n, int32_t rounds_done) {
+  if (!c) return PR_E_ARG;
+  return seed_one(c, ranks, n, rounds_done);
+}
+
+int pr_checkpoint_save(pr_ctx* c, const char* path) {
+  if (!c || !path) return c ? fail(c, PR_E_ARG, "null path") : PR_E_ARG;
+  int rc = gather_ranks(c);  // collective
+  if (rc) return rc;
+  if (c->opts.rank != 0) return PR_OK;
+  CkptHeader h{};
+  std::memcpy(h.magic, "PRMICKP1", 8);
+  h.version = 1;
+  h.flags = c->opts.flags & PR_F_NORMALIZED;
+  h.n = c->dg.n;
+  h.nnz = c->dg.nnz;
+  h.n_tot = c->dg.n_tot;
+  h.digest0 = c->dg.digest[0];
+  h.digest1 = c->dg.digest[1];
+  h.rounds = static_cast<int64_t>(c->dg.seeded ? c->seed_rounds : 0) + c->last_iters;
+  FILE* f = fopen(path, "wb");
+  if (!f) return fail(c, PR_E_IO, std::string("cannot open ") + path);
+  bool ok = fwrite(&h, sizeof(h), 1, f) == 1;
+  if (h.n) ok = ok && fwrite(c->h_ranks.data(), 8, h.n, f) == h.n;
+  ok = (fclose(f) == 0) && ok;
+  return ok ? PR_OK : fail(c, PR_E_IO, std::string("short write: ") + path);
+}
+
+int pr_checkpoint_load(pr_ctx* c, const char* path) {
+  if (!c || !path) return c ? fail(c, PR_E_ARG, "null path") : PR_E_ARG;
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail(c, PR_E_IO, std::string("cannot open ") + path);
+  CkptHeader h{};
+  bool ok = fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, "PRMICKP1", 8) == 0 && h.version == 1;
+  std::vector<double> r;
+  if (ok && h.n == c->dg.n) {
+    r.resize(h.n);
+    ok = h.n == 0 || fread(r.data(), 8, h.n, f) == h.n;
+  }
+  fclose(f);
+  if (!ok) return fail(c, PR_E_IO, std::string("not a prmi355x checkpoint: ") + path);
+  if (h.n != c->dg.n || h.nnz != c->dg.nnz || h.n_tot != c->dg.n_tot ||
+      h.digest0 != c->dg.digest[0] || h.digest1 != c->dg.digest[1])
+    return fail(c, PR_E_ARG, "checkpoint belongs to another graph");
+  if (h.flags != (c->opts.flags & PR_F_NORMALIZED))
+    return fail(c, PR_E_ARG, "checkpoint normalization differs from this context's");
+  if (h.rounds < 0 || h.rounds > INT32_MAX) return fail(c, PR_E_ARG, "checkpoint round count");
+  if (h.rounds == 0) return seed_one(c, nullptr, 0, 0);  // round 0 = r^0: a fresh start
+  return seed_one(c, r.data(), r.size(), static_cast<int32_t>(h.rounds));
+}

@@ -109,6 +109,14 @@ struct DevGraph {
   uint32_t* indeg = nullptr;
   uint32_t* dang_w = nullptr;
   uint32_t* mapw = nullptr;       // [n] mapping pairs per page (nullptr: every page once)
+  // initial rank and damping base: 1.0 and 0.15 (PageRank.java:78, :143), or 1/N_tot and
+  // 0.15/N_tot with PR_F_NORMALIZED
+  double r0 = 1.0, base = 0.15;
+  // pr_set_ranks / checkpoint resume: runs start from these instead of r^0
+  bool seeded = false;
+  double* x_seed = nullptr;       // [X] x of the seed ranks (every rank's slots)
+  double* r_seed = nullptr;       // [lrows] the seed ranks of this rank's rows
+  IterState seed_state{};
   double* x_init = nullptr;
   double* xbuf[2] = {nullptr, nullptr};
   double* r_loc[2] = {nullptr, nullptr};
@@ -133,6 +141,7 @@ struct BuildInput {
   int scale = 0;
   int edge_factor = 0;
   uint64_t seed = 0;
+  bool normalized = false;          // PR_F_NORMALIZED: r^0 = 1/N_tot, base 0.15/N_tot
 };
 
 // Builds the per-rank CSR and all iteration buffers.  Returns 0 or a PR_E_* code.
@@ -153,6 +162,9 @@ double* dev_x_out(DevGraph* g, int t);
 // Scatter this rank's final ranks into r_full (by original id; zeros elsewhere).
 // iterations == 0 reproduces ranks = 1.0 on sources (PageRank.java:76-83).
 int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s);
+// Seed the next runs with ranks by original id (host, n entries; 0 = undefined): x, this
+// rank's row ranks and the exact dangling mass of the seed.  ranks == nullptr clears it.
+int dev_seed_state(DevGraph* g, const double* ranks, hipStream_t s, std::string* err);
 // Host copy of this rank's pull CSR (single-rank graphs: internal ids, sources ascending).
 // Top-K candidates of this rank (PageRank.java:167-189): every mapped page whose rank is >=
 // the k-th largest rank counted with mapping-pair multiplicity among this rank's pages

@@ -183,6 +183,7 @@ struct RowArgs {
   uint64_t* shards;
   uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
   uint32_t dbg;              // PR_DBG timing experiments: 16 no LDS adds, 32 no epilogue, 64 no pieces
+  double base, r0;           // damping base (0.15) and initial rank (1.0), or their /N_tot forms
 };
 
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
@@ -210,8 +211,9 @@ __device__ __forceinline__ void row_finish(const RowArgs& A, double a, uint32_t 
   double r = 0.0;
   uint32_t w = 0;
   if (leader) {
-    // PageRank.java:143  0.15 + (sum + addthis) * 0.85, unfused
-    r = c > 0.0 ? __dadd_rn(0.15, __dmul_rn(__dadd_rn(c, a), 0.85)) : 0.0;
+    // PageRank.java:143  0.15 + (sum + addthis) * 0.85, unfused (base = 0.15 / N_tot when
+    // normalized)
+    r = c > 0.0 ? __dadd_rn(A.base, __dmul_rn(__dadd_rn(c, a), 0.85)) : 0.0;
     if (cls == 0)
       A.x_out[xslot_of(A, row)] = r / static_cast<double>(mt);  // :113  rank / urlCount
     else
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     const uint32_t row = rb0 + tid + q * BLOCK;
     mt[q] = row < rb1 ? A.meta[row] : 0u;
     ro[q] = 0.0;
-    if (MODE == 2 && row < rb1) ro[q] = A.r_old ? A.r_old[row] : 1.0;
+    if (MODE == 2 && row < rb1) ro[q] = A.r_old ? A.r_old[row] : A.r0;
   }
   // run lengths of the block's streams -> exclusive prefix pre[] (SPT streams per thread)
   const uint32_t NS = A.NS;
@@ -714,7 +716,7 @@ __global__ __launch_bounds__(BLOCK) void reduce_shards(uint64_t* shards, uint64_
 
 // Combine the p rank records (integer sums: order-free, exact) -> next round's addthis.
 __global__ void finalize_round(const uint64_t* rec_all, int p, int t, uint64_t n_tot,
-                               uint64_t extra_resid, int tracked, IterState* st) {
+                               uint32_t extra_pages, double r0, int tracked, IterState* st) {
   if (threadIdx.x != 0) return;
   uint64_t dsum[SA_LIMBS] = {0}, res[SA_LIMBS] = {0}, rsum[SA_LIMBS] = {0};
   uint64_t dcnt = 0;
@@ -732,9 +734,13 @@ __global__ void finalize_round(const uint64_t* rec_all, int p, int t, uint64_t n
   st->dcnt = dcnt;
   if (dcnt == 0 && st->err_iter == 0) st->err_iter = t + 1;
   if (tracked) {
-    // whole units: 1.0 = 2^96 units = bit 0 of limb 3
-    res[3] += extra_resid & 0xFFFFFFFFull;
-    res[4] += extra_resid >> 32;
+    // round 1: the pages that are not rows drop from r0 to undefined, |dr| = r0 each
+    uint32_t c0, c1, c2, c3;
+    const int li = sa_chunks(r0, extra_pages, c0, c1, c2, c3);
+    if (li >= 0) {
+      const uint32_t cs[4] = {c0, c1, c2, c3};
+      for (int q = 0; q < 4 && li + q < SA_LIMBS; ++q) res[li + q] += cs[q];
+    }
     const double ra = sa_to_double_dev(res);
     const double rs = sa_to_double_dev(rsum);
     st->resid_abs = ra;
@@ -911,12 +917,45 @@ __device__ __forceinline__ uint32_t slice_of(const Layout& L, uint32_t k) {
   return ((k < L.nA ? k : k - L.R) / CHUNK) % NSLICE;
 }
 
+// x of every column from r^0 (r0 on all sources) or, for a seed, from ranks by original id
 __global__ void k_x_init(const uint32_t* perm, const uint32_t* outdeg, uint32_t n, Layout L,
-                         double* x_init) {
+                         double r0, const double* ranks, double* x_init) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const bool col = k < L.nA || (k >= L.R && k < L.R + L.nC);
-  if (col) x_init[xpos(L, k)] = 1.0 / static_cast<double>(outdeg[perm[k]]);
+  const uint32_t v = perm[k];
+  if (col) x_init[xpos(L, k)] = (ranks ? ranks[v] : r0) / static_cast<double>(outdeg[v]);
+}
+
+// seed ranks of this rank's rows
+__global__ void k_r_seed(const uint32_t* perm, const double* ranks, uint32_t lrows, Layout L,
+                         double* r_seed) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l < lrows) r_seed[l] = ranks[perm[row_of(L, l)]];
+}
+
+// exact dangling mass + defined-entry count of a seed (PageRank.java:125-134) -> rec
+__global__ __launch_bounds__(BLOCK) void k_seed_dangling(const double* ranks, const uint32_t* dang_w,
+                                                         uint32_t n, uint64_t* rec) {
+  __shared__ uint64_t lds[BLOCK / 64][REC_WORDS];
+  for (int i = threadIdx.x; i < (BLOCK / 64) * REC_WORDS; i += BLOCK) (&lds[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t v = blockIdx.x * BLOCK + threadIdx.x;
+  const double r = v < n ? ranks[v] : 0.0;
+  const uint32_t w = v < n ? dang_w[v] : 0u;
+  uint64_t* lw = lds[threadIdx.x >> 6];
+  uint32_t c0, c1, c2, c3;
+  const int li = sa_chunks(r, w, c0, c1, c2, c3);
+  wave_accum_sa(lw, REC_DSUM, li, c0, c1, c2, c3);
+  const uint64_t cnt = wave_sum_u64((r > 0.0) ? w : 0u);
+  if ((threadIdx.x & 63) == 0) lw[REC_DCNT] += cnt;
+  __syncthreads();
+  if (threadIdx.x < REC_WORDS) {
+    uint64_t t = 0;
+    for (int q = 0; q < BLOCK / 64; ++q) t += lds[q][threadIdx.x];
+    if (t) atomicAdd(reinterpret_cast<unsigned long long*>(&rec[threadIdx.x]),
+                     static_cast<unsigned long long>(t));
+  }
 }
 
 // ---- slice streams -----------------------------------------------------------------------
@@ -1219,9 +1258,9 @@ __global__ void k_scatter_ranks(const uint32_t* perm, const double* r_loc, uint3
   if (l < lrows) r_full[perm[row_of(L, l)]] = r_loc[l];
 }
 
-__global__ void k_sources_one(const uint32_t* outdeg, uint32_t n, double* r_full) {
+__global__ void k_sources_one(const uint32_t* outdeg, uint32_t n, double r0, double* r_full) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v < n) r_full[v] = outdeg[v] ? 1.0 : 0.0;
+  if (v < n) r_full[v] = outdeg[v] ? r0 : 0.0;
 }
 
 // ---- top-K selection (PageRank.java:167-189 join(mappings) + sortByKey(false) + take(k)) --
@@ -1329,6 +1368,7 @@ void dev_free(DevGraph* g) {
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
   F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->mapw);
+  F(g->x_seed); F(g->r_seed);
   const int p = g->p, rank = g->rank;
   *g = DevGraph();
   g->p = p;
@@ -1371,6 +1411,14 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   g->n = n;
   g->m_raw = m;
   g->n_tot = in.n_tot;
+  if (in.normalized) {
+    if (in.n_tot == 0) {
+      if (err) *err = "normalized ranks need N_tot > 0 (an empty mapping divides by zero)";
+      return PR_E_ARG;
+    }
+    g->r0 = 1.0 / static_cast<double>(in.n_tot);
+    g->base = 0.15 / static_cast<double>(in.n_tot);
+  }
   const int nb = in.rmat ? std::max(1, in.scale) : bits_for(n);
   // raw edge keys (dst, src) take 2*nb bits
   if (2 * nb > 64) {
@@ -1515,7 +1563,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   HIPTRY(hipMemsetAsync(g->x_init, 0, 8 * (g->X ? g->X : 1), s));
   HIPTRY(hipMemsetAsync(g->xbuf[0], 0, 8 * (g->X ? g->X : 1), s));
   HIPTRY(hipMemsetAsync(g->xbuf[1], 0, 8 * (g->X ? g->X : 1), s));
-  if (n) hipLaunchKernelGGL(k_x_init, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->perm, g->outdeg, n, L, g->x_init);
+  if (n) hipLaunchKernelGGL(k_x_init, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->perm, g->outdeg, n, L, g->r0, static_cast<const double*>(nullptr), g->x_init);
   uint32_t* inv = vid;  // reuse: n entries
   if (n) hipLaunchKernelGGL(k_inverse, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->perm, n, inv);
 
@@ -1729,8 +1777,13 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
 int dev_reset_state(DevGraph* g, hipStream_t s) {
   std::string* err = nullptr;
   IterState st{};
-  st.a = g->n_tot ? static_cast<double>(g->W0) / static_cast<double>(g->n_tot) : 0.0;
-  st.dcnt = g->W0;
+  if (g->seeded) {
+    st = g->seed_state;
+  } else {
+    // :125-135 round 1: W0 dangling entries at r0 each (one exact product), / N_tot
+    st.a = g->n_tot ? (static_cast<double>(g->W0) * g->r0) / static_cast<double>(g->n_tot) : 0.0;
+    st.dcnt = g->W0;
+  }
   HIPTRY(hipMemcpyAsync(g->state, &st, sizeof(st), hipMemcpyHostToDevice, s));
   HIPTRY(hipMemsetAsync(g->shards, 0, 8ull * NSHARD * REC_WORDS, s));
   return PR_OK;
@@ -1762,7 +1815,7 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
 int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev0,
                       hipEvent_t ev1) {
   std::string* err = nullptr;
-  const double* x_in = t == 1 ? g->x_init : g->xbuf[t & 1];
+  const double* x_in = t == 1 ? (g->seeded ? g->x_seed : g->x_init) : g->xbuf[t & 1];
   StreamArgs S{};
   S.col = g->col;
   S.col16 = g->col16;
@@ -1790,7 +1843,9 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.lrows = g->lrows;
   A.meta = g->meta;
   A.x_out = dev_x_out(g, t) + static_cast<uint64_t>(g->rank) * g->maxA;
-  A.r_old = t == 1 ? nullptr : g->r_loc[(t - 1) & 1];
+  A.r_old = t == 1 ? (g->seeded ? g->r_seed : nullptr) : g->r_loc[(t - 1) & 1];
+  A.base = g->base;
+  A.r0 = g->r0;
   A.r_out = g->r_loc[t & 1];
   A.st = g->state;
   A.shards = g->shards;
@@ -1822,8 +1877,9 @@ int dev_round_finalize(DevGraph* g, int t, bool tracked, hipStream_t s) {
   std::string* err = nullptr;
   const uint64_t* rec = g->p > 1 ? g->rec_all : g->rec_local;
   // round 1 starts from r^0 == 1 on every page: pages that are not rows drop to 0 (|dr|=1)
-  const uint64_t extra = (t == 1 && g->rank == 0) ? static_cast<uint64_t>(g->n - g->R) : 0;
-  hipLaunchKernelGGL(finalize_round, dim3(1), dim3(64), 0, s, rec, g->p, t, g->n_tot, extra, tracked ? 1 : 0, g->state);
+  // (a seed has no defined page outside the rows: nothing drops)
+  const uint32_t extra = (t == 1 && g->rank == 0 && !g->seeded) ? g->n - g->R : 0u;
+  hipLaunchKernelGGL(finalize_round, dim3(1), dim3(64), 0, s, rec, g->p, t, g->n_tot, extra, g->r0, tracked ? 1 : 0, g->state);
   HIPTRY(hipGetLastError());
   return PR_OK;
 }
@@ -1832,12 +1888,51 @@ int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s) {
   std::string* err = nullptr;
   const uint32_t n = g->n;
   HIPTRY(hipMemsetAsync(g->r_full, 0, 8ull * (n ? n : 1), s));
-  if (iterations == 0) {
-    if (g->rank == 0 && n) hipLaunchKernelGGL(k_sources_one, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->outdeg, n, g->r_full);
+  if (iterations == 0 && g->seeded) {  // a seeded context that ran no round: the seed
+    if (g->lrows) hipLaunchKernelGGL(k_scatter_ranks, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->perm, static_cast<const double*>(g->r_seed), g->lrows, layout_of(g), g->r_full);
+  } else if (iterations == 0) {
+    if (g->rank == 0 && n) hipLaunchKernelGGL(k_sources_one, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->outdeg, n, g->r0, g->r_full);
   } else if (g->lrows) {
     hipLaunchKernelGGL(k_scatter_ranks, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->perm, g->r_loc[iterations & 1], g->lrows, layout_of(g), g->r_full);
   }
   HIPTRY(hipGetLastError());
+  return PR_OK;
+}
+
+int dev_seed_state(DevGraph* g, const double* ranks, hipStream_t s, std::string* err) {
+  g->seeded = false;
+  if (!ranks) return PR_OK;
+  const uint32_t n = g->n;
+  const Layout L = layout_of(g);
+  if (!g->x_seed) TRY(dmalloc(&g->x_seed, g->X, err));
+  if (!g->r_seed) TRY(dmalloc(&g->r_seed, g->lrows, err));
+  HIPTRY(hipMemsetAsync(g->x_seed, 0, 8ull * (g->X ? g->X : 1), s));
+  if (n) HIPTRY(hipMemcpyAsync(g->r_full, ranks, 8ull * n, hipMemcpyHostToDevice, s));
+  uint64_t* rec = nullptr;
+  IterState* st = nullptr;
+  TRY(dmalloc(&rec, REC_WORDS, err));
+  if (dmalloc(&st, 1, err) != PR_OK) {
+    (void)hipFree(rec);
+    return PR_E_OOM;
+  }
+  struct Free {
+    void *a, *b;
+    ~Free() { (void)hipFree(a); (void)hipFree(b); }
+  } fr{rec, st};
+  HIPTRY(hipMemsetAsync(rec, 0, 8ull * REC_WORDS, s));
+  HIPTRY(hipMemsetAsync(st, 0, sizeof(IterState), s));
+  if (n) {
+    hipLaunchKernelGGL(k_x_init, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->perm, g->outdeg, n, L, g->r0, static_cast<const double*>(g->r_full), g->x_seed);
+    hipLaunchKernelGGL(k_seed_dangling, dim3(grid_for(n)), dim3(BLOCK), 0, s, static_cast<const double*>(g->r_full), static_cast<const uint32_t*>(g->dang_w), n, rec);
+  }
+  if (g->lrows) hipLaunchKernelGGL(k_r_seed, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->perm, static_cast<const double*>(g->r_full), g->lrows, L, g->r_seed);
+  // every rank sees the whole seed: the dangling record is complete on each (p = 1 here)
+  hipLaunchKernelGGL(finalize_round, dim3(1), dim3(64), 0, s, static_cast<const uint64_t*>(rec), 1, 0, g->n_tot, 0u, g->r0, 0, st);
+  HIPTRY(hipGetLastError());
+  HIPTRY(hipMemcpyAsync(&g->seed_state, st, sizeof(IterState), hipMemcpyDeviceToHost, s));
+  HIPTRY(hipStreamSynchronize(s));
+  g->seed_state.iter = 0;
+  g->seeded = true;
   return PR_OK;
 }
 

@@ -2,6 +2,11 @@
 // where no JVM is available.  Same job, same file contract, engine behind the C ABI.
 //
 //   pagerank [ARCS MAPPING [ITERATIONS]] [--out PATH] [--topk K] [--tol X] [--verbose]
+//            [--normalized] [--resume CKPT] [--checkpoint CKPT]
+//
+// --normalized, --resume and --checkpoint are not in the reference:
+// normalized ranks (r^0 = 1/N_tot, base 0.15/N_tot); continue from a checkpoint's ranks for
+// ITERATIONS more rounds; write the final ranks as a checkpoint.
 //
 // No positional arguments: reads ./wikipedia_arcs and ./wikipedia_mapping (the basenames of
 // the reference's hard-coded s3n inputs, :27,:30), runs 10 rounds (:92) and writes the top
@@ -25,6 +30,7 @@ static int die(pr_ctx* c, int rc) {
 
 int main(int argc, char** argv) {
   std::string arcs = "./wikipedia_arcs", mapping = "./wikipedia_mapping", out = "./topPage";
+  std::string resume, checkpoint;
   int iterations = 10, npos = 0;
   double tol = 0.0;
   pr_opts o;
@@ -35,8 +41,12 @@ int main(int argc, char** argv) {
     else if (a == "--topk" && i + 1 < argc) o.topk = static_cast<uint32_t>(atoi(argv[++i]));
     else if (a == "--tol" && i + 1 < argc) tol = atof(argv[++i]);
     else if (a == "--verbose") o.flags |= PR_F_VERBOSE;
+    else if (a == "--normalized") o.flags |= PR_F_NORMALIZED;
+    else if (a == "--resume" && i + 1 < argc) resume = argv[++i];
+    else if (a == "--checkpoint" && i + 1 < argc) checkpoint = argv[++i];
     else if (a == "-h" || a == "--help") {
-      printf("usage: %s [ARCS MAPPING [ITERATIONS]] [--out PATH] [--topk K] [--tol X] [--verbose]\n", argv[0]);
+      printf("usage: %s [ARCS MAPPING [ITERATIONS]] [--out PATH] [--topk K] [--tol X] [--verbose]\n"
+             "          [--normalized] [--resume CKPT] [--checkpoint CKPT]\n", argv[0]);
       return 0;
     } else {
       if (npos == 0) arcs = a;
@@ -50,9 +60,17 @@ int main(int argc, char** argv) {
   if (rc) return die(c, rc);
   rc = pr_ingest_files(c, arcs.c_str(), mapping.c_str());
   if (rc) return die(c, rc);
+  if (!resume.empty()) {
+    rc = pr_checkpoint_load(c, resume.c_str());
+    if (rc) return die(c, rc);
+  }
   pr_stats st;
   rc = pr_run(c, iterations, tol, &st);
   if (rc) return die(c, rc);
+  if (!checkpoint.empty()) {
+    rc = pr_checkpoint_save(c, checkpoint.c_str());
+    if (rc) return die(c, rc);
+  }
   if (o.flags & PR_F_VERBOSE)
     fprintf(stderr, "[prmi355x] %d rounds, %.3f ms/round, %.2f GTEPS, nnz=%llu\n", st.iterations,
             st.ms_per_iter, st.gteps, static_cast<unsigned long long>(st.nnz));

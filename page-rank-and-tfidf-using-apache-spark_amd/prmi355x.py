@@ -37,6 +37,7 @@ PR_DEVICE_FROM_RANK = -1
 PR_DEVICE_NONE = -2
 PR_F_TRACK_RESIDUAL = 0x1
 PR_F_VERBOSE = 0x2
+PR_F_NORMALIZED = 0x4
 
 
 # ---- the reference's failure modes ------------------------------------------------------
@@ -145,6 +146,9 @@ def lib():
         "pr_edge_digest": (I32, [P, P]),
         "pr_export_csr": (I32, [P, P, P, P, P, C.POINTER(U64), C.POINTER(U64)]),
         "pr_format_double": (I32, [D, C.c_char_p, SZ]),
+        "pr_set_ranks": (I32, [P, P, U64, I32]),
+        "pr_checkpoint_save": (I32, [P, C.c_char_p]),
+        "pr_checkpoint_load": (I32, [P, C.c_char_p]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)
@@ -254,6 +258,22 @@ class Engine:
         cnt = C.c_uint32(0)
         self._check(lib().pr_topk(self._h, k, _ptr(pair), _ptr(vid), _ptr(rk), C.byref(cnt)))
         return [(int(pair[i]), int(vid[i]), float(rk[i])) for i in range(cnt.value)]
+
+    # ---- resume ----
+    def set_ranks(self, ranks: Optional[np.ndarray], rounds_done: int = 0):
+        """Seed later runs with ranks (by vertex id) reached after rounds_done rounds;
+        None clears the seed."""
+        if ranks is None:
+            self._check(lib().pr_set_ranks(self._h, None, 0, 0))
+            return
+        r = np.ascontiguousarray(ranks, np.float64)
+        self._check(lib().pr_set_ranks(self._h, _ptr(r), len(r), rounds_done))
+
+    def checkpoint_save(self, path: str):
+        self._check(lib().pr_checkpoint_save(self._h, path.encode()))
+
+    def checkpoint_load(self, path: str):
+        self._check(lib().pr_checkpoint_load(self._h, path.encode()))
 
     def write_top_page(self, path: str = "./topPage"):
         self._check(lib().pr_write_top_page(self._h, path.encode()))

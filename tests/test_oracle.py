@@ -172,3 +172,17 @@ def test_java_double_to_string():
              1.5e300: "1.5E300", 0.0: "0.0"}
     for v, s in cases.items():
         assert L.java_double_to_string(v) == s
+
+
+def test_oracle_normalized_and_resume(oracle_mod):
+    """The oracle's extra options: normalized = plain / N_tot up to
+    rounding; T1 rounds then T2 from those ranks == T1 + T2 rounds, bit for bit."""
+    import numpy as np
+    O = oracle_mod
+    g = O.Graph.from_rmat(12, 16, 5)
+    plain = g.run(10)["ranks"]
+    norm = g.run(10, normalized=True)["ranks"]
+    assert np.allclose(norm * g.n_tot, plain, rtol=1e-12, atol=0)
+    r4 = g.run(4)["ranks"]
+    r10 = g.run(6, r_init=r4)["ranks"]
+    assert np.array_equal(r10.view(np.uint64), plain.view(np.uint64))
