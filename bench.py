@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rounds", type=int, default=2)
+    ap.add_argument("--cpu-rounds", type=int, default=40)   # ~10 s of host CPU work at scale 26
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
 
