@@ -198,6 +198,26 @@ int pr_edge_digest(pr_ctx* ctx, uint64_t digest_out[2]);
 int pr_export_csr(pr_ctx* ctx, uint64_t* row_ptr, uint32_t* col, uint32_t* outdeg,
                   uint32_t* dang_w, uint64_t* n, uint64_t* nnz);
 
+/* ---- the repository's second job: TF-IDF (Spark.java:22-173) ----------
+ * Input: the tab-separated dump Spark.java:26 reads (one document per line, title in column
+ * 1, text in column 3).  pr_tfidf_ingest_* cleans every text (:38-42), counts (word, title)
+ * pairs (:57-71), document frequencies (:75-93) and titleCount = distinct titles (:50-56)
+ * on the device; PR_E_PARSE where the reference dies with ArrayIndexOutOfBoundsException
+ * (a line without columns[1] or columns[3]; a title made only of commas, :106).
+ * pr_tfidf_lookup is idf.lookup(word) + the sort of :140-162: up to k rows (title index,
+ * tf * Math.log(titleCount / df) with integer division), tfidf descending, ties by the
+ * lowercased title up to its first comma.  pr_tfidf_write_output writes the ./output file
+ * of :164-171 ("total docs are N" + the first 100 `title\ttfidf` rows).  Per context;
+ * independent of the PageRank graph.  Needs a device. */
+int pr_tfidf_ingest_buffer(pr_ctx* ctx, const char* data, size_t len);
+int pr_tfidf_ingest_file(pr_ctx* ctx, const char* path);
+int pr_tfidf_info(pr_ctx* ctx, uint64_t* docs, uint64_t* words, uint64_t* pairs,
+                  uint64_t* tokens);
+int pr_tfidf_lookup(pr_ctx* ctx, const char* word, size_t wlen, uint32_t k,
+                    uint32_t* title_out, double* tfidf_out, uint32_t* count);
+int pr_tfidf_title(pr_ctx* ctx, uint32_t title, char* buf, size_t cap, size_t* len);
+int pr_tfidf_write_output(pr_ctx* ctx, const char* word, const char* path);
+
 /* Java Double.toString layout (PageRank.java:197 string concatenation). Returns length. */
 int pr_format_double(double v, char* buf, size_t cap);
 

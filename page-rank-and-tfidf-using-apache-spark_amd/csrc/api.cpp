@@ -44,6 +44,7 @@ struct pr_ctx {
   double ms_ingest = 0;
   std::vector<pr_ctx*> group;    // single-process rank group (pr_comm_init_local)
   int seed_rounds = 0;           // pr_set_ranks: rounds behind the seed (0 = no seed)
+  prmi::TfidfState tf;           // the TF-IDF job (Spark.java)
 };
 
 namespace {
@@ -404,6 +405,7 @@ void pr_destroy(pr_ctx* c) {
   if (c->has_device) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    prmi::tf_free(&c->tf);
     prmi::dev_free(&c->dg);
     for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -1026,4 +1028,138 @@ int pr_checkpoint_load(pr_ctx* c, const char* path) {
   if (h.rounds < 0 || h.rounds > INT32_MAX) return fail(c, PR_E_ARG, "checkpoint round count");
   if (h.rounds == 0) return seed_one(c, nullptr, 0, 0);  // round 0 = r^0: a fresh start
   return seed_one(c, r.data(), r.size(), static_cast<int32_t>(h.rounds));
+}
+
+// ---- TF-IDF (Spark.java:22-173) -----------------------------------------
+namespace {
+
+struct TfRow {
+  double v;
+  uint32_t title;
+  std::string key;  // lowercased title up to its first ',' (Spark.java:106, :155-156)
+  std::string full;
+};
+
+// Spark.java:120-162 for `word`: rows sorted by tfidf descending, then the lowercased
+// truncated title (Collections.sort is stable; Spark's lookup order is unspecified, so the
+// full title bytes decide the rest)
+int tf_rows(pr_ctx* c, const char* word, size_t wlen, std::vector<TfRow>* rows) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  if (!c->tf.ready) return fail(c, PR_E_ARG, "no TF-IDF input: call pr_tfidf_ingest_* first");
+  std::vector<uint32_t> titles, tfs;
+  uint32_t df = 0;
+  std::string err;
+  rc = prmi::tf_lookup(&c->tf, word, wlen, &titles, &tfs, &df, c->stream, &err);
+  if (rc) return fail(c, rc, "tfidf lookup: " + err);
+  rows->clear();
+  if (titles.empty()) return PR_OK;
+  // :130-131  Math.log(titleCount / dword): Long / Integer is an integer division
+  const double idf = std::log(static_cast<double>(static_cast<uint64_t>(c->tf.n_docs) / df));
+  for (size_t i = 0; i < titles.size(); ++i) {
+    TfRow r;
+    r.v = static_cast<double>(static_cast<int32_t>(tfs[i])) * idf;  // :131 int * double
+    r.title = titles[i];
+    r.full.assign(c->tf.titles, c->tf.title_off[r.title], c->tf.title_off[r.title + 1] - c->tf.title_off[r.title]);
+    const size_t comma = r.full.find(',');
+    r.key = r.full.substr(0, comma);
+    for (char& ch : r.key)
+      if (ch >= 'A' && ch <= 'Z') ch = static_cast<char>(ch | 0x20);
+    rows->push_back(std::move(r));
+  }
+  std::sort(rows->begin(), rows->end(), [](const TfRow& a, const TfRow& b) {
+    if (a.v != b.v) return a.v > b.v;
+    if (a.key != b.key) return a.key < b.key;
+    return a.full < b.full;
+  });
+  return PR_OK;
+}
+
+}  // namespace
+
+int pr_tfidf_ingest_buffer(pr_ctx* c, const char* data, size_t len) {
+  if (!c || (!data && len)) return c ? fail(c, PR_E_ARG, "bad buffer") : PR_E_ARG;
+  int rc = need_device(c);
+  if (rc) return rc;
+  prmi::TfidfError te;
+  std::string err;
+  rc = prmi::tf_ingest(&c->tf, data ? data : "", len, &te, c->stream, &err);
+  if (rc == PR_E_PARSE) {
+    prmi::tf_free(&c->tf);
+    return fail(c, PR_E_PARSE, "java.lang.ArrayIndexOutOfBoundsException: " + std::to_string(te.index) +
+                                   " (line " + std::to_string(te.line) + ")");
+  }
+  if (rc) {
+    prmi::tf_free(&c->tf);
+    return fail(c, rc, "tfidf ingest: " + err);
+  }
+  return PR_OK;
+}
+
+int pr_tfidf_ingest_file(pr_ctx* c, const char* path) {
+  if (!c || !path) return c ? fail(c, PR_E_ARG, "null path") : PR_E_ARG;
+  std::string d;
+  if (!read_file(path, &d)) return fail(c, PR_E_IO, std::string("cannot read ") + path);
+  return pr_tfidf_ingest_buffer(c, d.data(), d.size());
+}
+
+int pr_tfidf_info(pr_ctx* c, uint64_t* docs, uint64_t* words, uint64_t* pairs, uint64_t* tokens) {
+  if (!c) return PR_E_ARG;
+  if (!c->tf.ready) return fail(c, PR_E_ARG, "no TF-IDF input");
+  if (docs) *docs = c->tf.n_docs;
+  if (words) *words = c->tf.n_words;
+  if (pairs) *pairs = c->tf.n_pairs;
+  if (tokens) *tokens = c->tf.tokens;
+  return PR_OK;
+}
+
+int pr_tfidf_lookup(pr_ctx* c, const char* word, size_t wlen, uint32_t k, uint32_t* title_out,
+                    double* tfidf_out, uint32_t* count) {
+  if (!c || (!word && wlen)) return c ? fail(c, PR_E_ARG, "bad word") : PR_E_ARG;
+  std::vector<TfRow> rows;
+  int rc = tf_rows(c, word ? word : "", wlen, &rows);
+  if (rc) return rc;
+  const size_t n = std::min<size_t>(k, rows.size());
+  for (size_t i = 0; i < n; ++i) {
+    if (title_out) title_out[i] = rows[i].title;
+    if (tfidf_out) tfidf_out[i] = rows[i].v;
+  }
+  if (count) *count = static_cast<uint32_t>(n);
+  return PR_OK;
+}
+
+int pr_tfidf_title(pr_ctx* c, uint32_t t, char* buf, size_t cap, size_t* len) {
+  if (!c) return PR_E_ARG;
+  if (!c->tf.ready || t >= c->tf.n_docs) return fail(c, PR_E_ARG, "title index out of range");
+  const uint64_t a = c->tf.title_off[t], b = c->tf.title_off[t + 1];
+  if (len) *len = b - a;
+  if (buf && cap) {
+    const size_t m = std::min<size_t>(cap, b - a);
+    std::memcpy(buf, c->tf.titles.data() + a, m);
+  }
+  return PR_OK;
+}
+
+int pr_tfidf_write_output(pr_ctx* c, const char* word, const char* path) {
+  if (!c) return PR_E_ARG;
+  const char* w = word ? word : "cloud";  // :140 idf.lookup("cloud")
+  std::vector<TfRow> rows;
+  int rc = tf_rows(c, w, std::strlen(w), &rows);
+  if (rc) return rc;
+  std::string out = "total docs are " + std::to_string(c->tf.n_docs) + "\n";  // :165
+  char num[64];
+  for (size_t i = 0; i < rows.size() && i < 100; ++i) {  // :166-169
+    const std::string& t = rows[i].full;
+    prmi::java_double_to_string(rows[i].v, num, sizeof(num));
+    out += t.substr(0, t.find(','));  // kv[0] of "title,tfidf".split(",")
+    out += '\t';
+    out += num;
+    out += '\n';
+  }
+  FILE* f = fopen(path ? path : "./output", "wb");
+  if (!f) return fail(c, PR_E_IO, std::string("java.io.IOException: cannot open ") + (path ? path : "./output"));
+  const size_t wr = fwrite(out.data(), 1, out.size(), f);
+  const int cl = fclose(f);
+  if (wr != out.size() || cl != 0) return fail(c, PR_E_IO, "java.io.IOException: short write");
+  return PR_OK;
 }

@@ -171,6 +171,32 @@ int dev_seed_state(DevGraph* g, const double* ranks, hipStream_t s, std::string*
 // (ties at the boundary included), from r_full (call dev_scatter_ranks first).
 int dev_topk_candidates(DevGraph* g, uint64_t k, std::vector<uint32_t>* ids,
                         std::vector<double>* rs, hipStream_t s, std::string* err);
+// ---- TF-IDF job (tfidf.hip; Spark.java:22-173) ------------------------
+struct TfidfError {
+  bool failed = false;
+  int index = 0;       // the ArrayIndexOutOfBoundsException index (1, 3, or 0/1 at :83/:106)
+  uint64_t line = 0;   // 1-based line of the document that dies
+};
+struct TfidfState {
+  bool ready = false;
+  char* B = nullptr;               // the dump on the device (word bytes are read from it)
+  uint64_t bytes = 0, lines = 0, tokens = 0;
+  uint32_t n_docs = 0, n_words = 0, n_pairs = 0;  // titleCount (:56), distinct words, keys
+  uint64_t* w_off = nullptr;       // [n_words] first occurrence of each word in B
+  uint32_t* w_len = nullptr;
+  uint64_t* keys = nullptr;        // [n_pairs] (word << 32 | title), sorted: a word's keys
+  uint32_t* tf = nullptr;          //           are contiguous; tf = count (:66-71)
+  uint32_t* w_start = nullptr;     // [n_words + 1] first key of each word; df = the run
+  std::string titles;              // distinct titles, host (output strings)
+  std::vector<uint64_t> title_off;
+};
+void tf_free(TfidfState* t);
+int tf_ingest(TfidfState* t, const char* data, size_t len, TfidfError* te, hipStream_t s,
+              std::string* err);
+// the (title, tf) keys of `word` (exact bytes; words are lowercase) and its df
+int tf_lookup(TfidfState* t, const char* word, size_t wlen, std::vector<uint32_t>* titles,
+              std::vector<uint32_t>* tfs, uint32_t* df, hipStream_t s, std::string* err);
+
 // Text ingest on the device (ingest.hip): same result as ingest_text (host_graph.cpp).
 // PR_E_PARSE with *pe filled on a malformed line.
 int dev_ingest_text(const char* arcs, size_t alen, const char* map, size_t mlen, HostGraph* g,

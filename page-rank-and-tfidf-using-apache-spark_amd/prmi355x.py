@@ -149,6 +149,12 @@ def lib():
         "pr_set_ranks": (I32, [P, P, U64, I32]),
         "pr_checkpoint_save": (I32, [P, C.c_char_p]),
         "pr_checkpoint_load": (I32, [P, C.c_char_p]),
+        "pr_tfidf_ingest_buffer": (I32, [P, C.c_char_p, SZ]),
+        "pr_tfidf_ingest_file": (I32, [P, C.c_char_p]),
+        "pr_tfidf_info": (I32, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
+        "pr_tfidf_lookup": (I32, [P, C.c_char_p, SZ, U32, P, P, C.POINTER(U32)]),
+        "pr_tfidf_title": (I32, [P, U32, C.c_char_p, SZ, C.POINTER(SZ)]),
+        "pr_tfidf_write_output": (I32, [P, C.c_char_p, C.c_char_p]),
     }
     for name, (rt, args) in sig.items():
         f = getattr(L, name)
@@ -274,6 +280,33 @@ class Engine:
 
     def checkpoint_load(self, path: str):
         self._check(lib().pr_checkpoint_load(self._h, path.encode()))
+
+    # ---- TF-IDF job (Spark.java) ----
+    def tfidf_ingest(self, data: bytes):
+        self._check(lib().pr_tfidf_ingest_buffer(self._h, data, len(data)))
+
+    def tfidf_info(self) -> Dict[str, int]:
+        v = [C.c_uint64(0) for _ in range(4)]
+        self._check(lib().pr_tfidf_info(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("docs", "words", "pairs", "tokens"), (x.value for x in v)))
+
+    def tfidf_title(self, t: int) -> bytes:
+        ln = C.c_size_t(0)
+        self._check(lib().pr_tfidf_title(self._h, t, None, 0, C.byref(ln)))
+        buf = C.create_string_buffer(max(ln.value, 1))
+        self._check(lib().pr_tfidf_title(self._h, t, buf, ln.value, C.byref(ln)))
+        return buf.raw[:ln.value]
+
+    def tfidf_lookup(self, word: bytes, k: int = 100) -> List[Tuple[bytes, float]]:
+        t = np.zeros(max(k, 1), np.uint32)
+        v = np.zeros(max(k, 1), np.float64)
+        cnt = C.c_uint32(0)
+        self._check(lib().pr_tfidf_lookup(self._h, word, len(word), k, _ptr(t), _ptr(v),
+                                          C.byref(cnt)))
+        return [(self.tfidf_title(int(t[i])), float(v[i])) for i in range(cnt.value)]
+
+    def tfidf_write_output(self, word: Optional[bytes] = None, path: str = "./output"):
+        self._check(lib().pr_tfidf_write_output(self._h, word, path.encode()))
 
     def write_top_page(self, path: str = "./topPage"):
         self._check(lib().pr_write_top_page(self._h, path.encode()))

@@ -147,3 +147,44 @@ def big_text(seed: int, pages: int, arcs: int) -> Tuple[bytes, bytes]:
     m2[:, 0:7], m2[:, 7], m2[:, 8:13], m2[:, 13:20] = digits(two), 9, list(b"Alt  "), digits(two)
     m2[:, 20], m2[:, 21] = ord("y"), 10
     return a.tobytes(), m1.tobytes() + m2.tobytes()
+
+
+def tfidf_dump(seed: int, docs: int = 2000, words_per_doc: int = 60) -> bytes:
+    """Stand-in for the Wikipedia dump Spark.java:26 reads (absent from the reference):
+    `id \\t title \\t date \\t text` lines with HTML tags, literal backslash-n sequences,
+    digits, punctuation, mixed case, titles with commas and repeated titles, some empty
+    texts and extra columns; "cloud" is common."""
+    rng = random.Random(seed)
+    vocab = ["cloud", "Cloud", "CLOUD", "computing", "storm", "rain", "sky", "data", "the",
+             "of", "and", "strife", "oort", "st", "server", "alpha", "beta", "gamma"] + \
+            ["w" + "".join(chr(97 + (i // 26 ** q) % 26) for q in range(3)) for i in range(3000)]
+    extra = ["<ref name=x>", "</ref>", "<b>", "</b>", "\\n", "\\n\\n", "1999", "3rd", "--",
+             "(", ")", "e.g.", "&amp;", "<", ">", "x<y", "a\\b", "\\", "n"]
+    titles = ["Page %d" % i for i in range(docs)]
+    for i in range(0, docs, 17):
+        titles[i] = "St. Cloud, Place %d" % (i % 5)          # truncated at ',' -> "St. Cloud"
+    for i in range(3, docs, 41):
+        titles[i] = titles[i - 1]                             # repeated titles merge
+    lines = []
+    for i in range(docs):
+        toks = []
+        for _ in range(rng.randint(0, words_per_doc)):
+            r = rng.random()
+            if r < 0.12:
+                toks.append(rng.choice(extra))
+            elif r < 0.2:
+                toks.append(rng.choice(["cloud", "Cloud"]))
+            else:
+                toks.append(rng.choice(vocab))
+        sep = rng.choice([" ", "  ", ", ", ".", " - "])
+        text = sep.join(toks)
+        if rng.random() < 0.05:
+            text = ""
+        if rng.random() < 0.1:
+            text = " " + text
+        cols = [str(100000 + i), titles[i], "2015-0%d" % rng.randint(1, 9), text]
+        if rng.random() < 0.05 or not text:   # an empty text needs a later field to exist
+            cols.append("extra column")
+        lines.append("\t".join(cols))
+    term = rng.choice(["\n", "\r\n"])
+    return (term.join(lines) + (term if rng.random() < 0.8 else "")).encode()
