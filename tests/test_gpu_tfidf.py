@@ -94,3 +94,21 @@ def test_idf_is_integer_division(P):
     assert eng.tfidf_lookup(b"a") == [(b"X", 0.0), (b"Y", 0.0)]
     assert eng.tfidf_lookup(b"c") == [(b"Z", math.log(3))]
     assert eng.tfidf_lookup(b"b") == [(b"X", 0.0), (b"Z", 0.0)]   # ties: by title
+
+
+def test_tfidf_cli_contract(P, tmp_path):
+    """`_build/tfidf DUMP --out PATH` (Spark.main's file contract) writes the oracle's file;
+    a malformed dump exits 1 with the Java exception on stderr."""
+    import os
+    import subprocess
+    cli = os.path.join(os.path.dirname(P.LIB_PATH), "tfidf")
+    data = G.tfidf_dump(7, docs=800)
+    (tmp_path / "data").write_bytes(data)
+    subprocess.run([cli, str(tmp_path / "data"), "--out", str(tmp_path / "output")],
+                   check=True, timeout=120)
+    assert (tmp_path / "output").read_bytes() == T.output(data)
+    (tmp_path / "bad").write_bytes(b"1\tA\tx\ty\nlonely\n")
+    r = subprocess.run([cli, str(tmp_path / "bad"), "--out", str(tmp_path / "o2")],
+                       capture_output=True, timeout=120)
+    assert r.returncode == 1 and b"ArrayIndexOutOfBoundsException: 1" in r.stderr
+    assert not (tmp_path / "o2").exists()
