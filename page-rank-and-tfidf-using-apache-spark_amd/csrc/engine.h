@@ -57,7 +57,10 @@ struct Tuning {
   uint32_t qh = 458752; // PR_QH: L2-hot segment length per slice after the LDS blocks (3.5 MiB)
   int nlds = 16;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
-  int nt = 0;           // PR_NT: non-temporal loads for the streamed arrays (slower: 3.8 vs 6 TB/s)
+  // PR_NT: cache policy of the stream launch's streamed operands: 1 non-temporal loads
+  // (slower), 2 non-temporal piece stores (faster: they no longer evict x from L2), 3 both
+  int nt = 2;
+  int rnt = 0;          // PR_RNT: row launch, 1 non-temporal piece loads, 2 non-temporal x'
   uint32_t hot_lds = 20480;  // PR_HOTLDS: LDS block length (x entries, capped by the staging room)
   uint32_t colmask = 0xFFFFFFFFu;  // PR_COLMASK: timing-only gather working-set restriction
   int dbg = 0;          // PR_DBG: timing-only experiments in the stream kernel (see StreamArgs)
