@@ -55,7 +55,7 @@ struct IterState {
 
 struct Tuning {
   uint32_t qh = 458752; // PR_QH: L2-hot segment length per slice after the LDS blocks (3.5 MiB)
-  int nlds = 16;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
+  int nlds = 18;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
   // PR_NT: cache policy of the stream launch's streamed operands: 1 non-temporal loads
   // (slower), 2 non-temporal piece stores (faster: they no longer evict x from L2), 3 both

@@ -582,7 +582,10 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       const uint32_t hb = A.hot_base[j] + gi * A.H;
       __syncthreads();  // every wave is done with the previous block
       if (te > tb) {
-        for (uint32_t i = threadIdx.x; i < A.H; i += blockDim.x) hot[i] = x[hb + i];
+        for (uint32_t i = threadIdx.x; i < A.H; i += blockDim.x) {
+          if constexpr ((NT & 4) != 0) hot[i] = __builtin_nontemporal_load(x + hb + i);
+          else hot[i] = x[hb + i];
+        }
         if (threadIdx.x == 0) hot[A.H] = 0.0;  // the padding column
       }
       __syncthreads();
@@ -1818,13 +1821,15 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
     for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<0>),
                           reinterpret_cast<const void*>(&spmv_stream<1>),
                           reinterpret_cast<const void*>(&spmv_stream<2>),
-                          reinterpret_cast<const void*>(&spmv_stream<3>)})
+                          reinterpret_cast<const void*>(&spmv_stream<3>),
+                          reinterpret_cast<const void*>(&spmv_stream<6>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   if (g->tune.nt == 1) hipLaunchKernelGGL((spmv_stream<1>), gr, bl, lds, s, A);
   else if (g->tune.nt == 2) hipLaunchKernelGGL((spmv_stream<2>), gr, bl, lds, s, A);
   else if (g->tune.nt == 3) hipLaunchKernelGGL((spmv_stream<3>), gr, bl, lds, s, A);
+  else if (g->tune.nt == 6) hipLaunchKernelGGL((spmv_stream<6>), gr, bl, lds, s, A);
   else hipLaunchKernelGGL((spmv_stream<0>), gr, bl, lds, s, A);
 }
 
