@@ -57,10 +57,9 @@ struct Tuning {
   uint32_t qh = 458752; // PR_QH: L2-hot segment length per slice after the LDS blocks (3.5 MiB)
   int nlds = 18;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
-  // PR_NT: cache policy of the stream launch's streamed operands: 1 non-temporal loads
-  // (slower), 2 non-temporal piece stores (faster: they no longer evict x from L2), 3 both
+  // PR_NT: 2 = non-temporal piece stores (they stop evicting x from the L2s: +3 %), 0 =
+  // regular stores.  Non-temporal stream loads and LDS fills were measured slower.
   int nt = 2;
-  int rnt = 0;          // PR_RNT: row launch, 1 non-temporal piece loads, 2 non-temporal x'
   uint32_t hot_lds = 20480;  // PR_HOTLDS: LDS block length (x entries, capped by the staging room)
   uint32_t colmask = 0xFFFFFFFFu;  // PR_COLMASK: timing-only gather working-set restriction
   int dbg = 0;          // PR_DBG: timing-only experiments in the stream kernel (see StreamArgs)

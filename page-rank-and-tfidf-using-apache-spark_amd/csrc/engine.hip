@@ -184,7 +184,6 @@ struct RowArgs {
   uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
   uint32_t dbg;              // PR_DBG timing experiments: 16 no LDS adds, 32 no epilogue, 64 no pieces
   double base, r0;           // damping base (0.15) and initial rank (1.0), or their /N_tot forms
-  uint32_t rnt;              // PR_RNT experiments: 1 non-temporal piece loads, 2 non-temporal x'
 };
 
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
@@ -194,13 +193,6 @@ __device__ __forceinline__ uint32_t xslot_of(const RowArgs& A, uint32_t l) {
   return (sl / A.p) * A.SL + (c / NSLICE) * CHUNK + (l % CHUNK);
 }
 
-// Streamed (read-once) operands: non-temporal loads (NT = 1) were measured slower than
-// regular loads for streams (3.8 vs 6.0 TB/s, scripts/probes/stream_probe.hip).
-template <int NT, class T>
-__device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr ((NT & 1) != 0) return __builtin_nontemporal_load(p);
-  else return *p;
-}
 
 // Epilogue of one row (leader = the row exists): r', x' or the row's dangling weight, and in
 // tracked mode r'; the exact partials (dangling mass + count for class-B rows; residual +
@@ -216,11 +208,7 @@ __device__ __forceinline__ void row_finish(const RowArgs& A, double a, uint32_t 
     // normalized)
     r = c > 0.0 ? __dadd_rn(A.base, __dmul_rn(__dadd_rn(c, a), 0.85)) : 0.0;
     if (cls == 0)
-    {
-      const double xv = r / static_cast<double>(mt);  // :113  rank / urlCount
-      if (A.rnt & 2u) __builtin_nontemporal_store(xv, A.x_out + xslot_of(A, row));
-      else A.x_out[xslot_of(A, row)] = xv;
-    }
+      A.x_out[xslot_of(A, row)] = r / static_cast<double>(mt);  // :113  rank / urlCount
     else
       w = mt;
     if (MODE >= 1) A.r_out[row] = r;
@@ -351,13 +339,8 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     locate(pos, pc);
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
-      if (A.rnt & 1u) {
-        vv[u] = __builtin_nontemporal_load(A.partial + pc[u]);
-        rr[u] = __builtin_nontemporal_load(A.roff + pc[u]);
-      } else {
-        vv[u] = A.partial[pc[u]];
-        rr[u] = A.roff[pc[u]];
-      }
+      vv[u] = A.partial[pc[u]];
+      rr[u] = A.roff[pc[u]];
     }
   };
   auto add = [&](uint32_t pos, const double (&vv)[EPR], const uint32_t (&rr)[EPR]) {
@@ -555,15 +538,15 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // groups are padded to whole tasks: these loads never leave the stream buffers
     if (lds_task) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
-      cn[0] = ld_stream<NT>(cp);
-      cn[1] = ld_stream<NT>(cp + 1);
+      cn[0] = cp[0];
+      cn[1] = cp[1];
     } else {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) cn[q] = ld_stream<NT>(cp + q);
+      for (int q = 0; q < 4; ++q) cn[q] = cp[q];
     }
     const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
-    bnx = ld_stream<NT>(bits + so / EPL);
+    bnx = bits[so / EPL];
     tpn = tpa[tt];
   };
   // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
@@ -582,10 +565,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       const uint32_t hb = A.hot_base[j] + gi * A.H;
       __syncthreads();  // every wave is done with the previous block
       if (te > tb) {
-        for (uint32_t i = threadIdx.x; i < A.H; i += blockDim.x) {
-          if constexpr ((NT & 4) != 0) hot[i] = __builtin_nontemporal_load(x + hb + i);
-          else hot[i] = x[hb + i];
-        }
+        for (uint32_t i = threadIdx.x; i < A.H; i += blockDim.x) hot[i] = x[hb + i];
         if (threadIdx.x == 0) hot[A.H] = 0.0;  // the padding column
       }
       __syncthreads();
@@ -1417,7 +1397,6 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.qh = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_QH", static_cast<int>(T.qh))));
   T.seg = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_SEG", static_cast<int>(T.seg))));
   T.nt = env_int("PR_NT", T.nt);
-  T.rnt = env_int("PR_RNT", T.rnt);
   T.hot_lds = static_cast<uint32_t>(std::max(0, std::min(20480, env_int("PR_HOTLDS", static_cast<int>(T.hot_lds)))));
   T.dbg = env_int("PR_DBG", 0);
   T.nlds = std::max(0, std::min(64, env_int("PR_NLDS", T.nlds)));
@@ -1569,14 +1548,9 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   const Layout L = layout_of(g);
 
   // ---- x vectors ------------------------------------------------------------------------
-  if (env_int("PR_XUNCACHED", 0)) {  // experiment: x in uncached device memory (32-B reads)
-    for (double** px : {&g->x_init, &g->xbuf[0], &g->xbuf[1]})
-      HIPTRY(hipExtMallocWithFlags(reinterpret_cast<void**>(px), 8 * (g->X ? g->X : 1), hipDeviceMallocUncached));
-  } else {
-    TRY(dmalloc(&g->x_init, g->X, err));
-    TRY(dmalloc(&g->xbuf[0], g->X, err));
-    TRY(dmalloc(&g->xbuf[1], g->X, err));
-  }
+  TRY(dmalloc(&g->x_init, g->X, err));
+  TRY(dmalloc(&g->xbuf[0], g->X, err));
+  TRY(dmalloc(&g->xbuf[1], g->X, err));
   HIPTRY(hipMemsetAsync(g->x_init, 0, 8 * (g->X ? g->X : 1), s));
   HIPTRY(hipMemsetAsync(g->xbuf[0], 0, 8 * (g->X ? g->X : 1), s));
   HIPTRY(hipMemsetAsync(g->xbuf[1], 0, 8 * (g->X ? g->X : 1), s));
@@ -1819,17 +1793,11 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   static bool attr_set = false;  // allow the >64 KB dynamic LDS request
   if (!attr_set) {
     for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<0>),
-                          reinterpret_cast<const void*>(&spmv_stream<1>),
-                          reinterpret_cast<const void*>(&spmv_stream<2>),
-                          reinterpret_cast<const void*>(&spmv_stream<3>),
-                          reinterpret_cast<const void*>(&spmv_stream<6>)})
+                          reinterpret_cast<const void*>(&spmv_stream<2>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  if (g->tune.nt == 1) hipLaunchKernelGGL((spmv_stream<1>), gr, bl, lds, s, A);
-  else if (g->tune.nt == 2) hipLaunchKernelGGL((spmv_stream<2>), gr, bl, lds, s, A);
-  else if (g->tune.nt == 3) hipLaunchKernelGGL((spmv_stream<3>), gr, bl, lds, s, A);
-  else if (g->tune.nt == 6) hipLaunchKernelGGL((spmv_stream<6>), gr, bl, lds, s, A);
+  if (g->tune.nt == 2) hipLaunchKernelGGL((spmv_stream<2>), gr, bl, lds, s, A);
   else hipLaunchKernelGGL((spmv_stream<0>), gr, bl, lds, s, A);
 }
 
@@ -1860,7 +1828,6 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.partial = g->partial;
   A.roff = g->roff;
   A.dbg = static_cast<uint32_t>(g->tune.dbg);
-  A.rnt = static_cast<uint32_t>(g->tune.rnt);
   A.NS = g->n_streams;
   A.nbA = g->nb_rows_a;
   A.lA = g->lA;
