@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Soak test (GPU): many R-MAT graphs of mixed scale / edge factor / seed / rank count and
+stream geometry (LDS block size, segments) against the exact oracle.  Prints one line per
+case; exits non-zero at the first mismatch.  usage: scripts/soak.py [cases=60]"""
+import os
+import random
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CASE = r'''
+import os, sys, numpy as np
+sys.path[:0] = [os.path.join(%(root)r, d) for d in ("page-rank-and-tfidf-using-apache-spark_amd", "oracle", "tests")]
+import prmi355x as P, oracle as O, parity
+scale, ef, seed, p, T = %(scale)d, %(ef)d, %(seed)d, %(p)d, %(T)d
+exp = O.Graph.from_rmat(scale, ef, seed).run(T)["ranks"]
+if p == 1:
+    e = P.Engine(); e.generate_rmat(scale, ef, seed); e.run(T); got = e.ranks()
+else:
+    g = P.LocalGroup(p); g.each("generate_rmat", scale, ef, seed); g.run(T); got = g.members[0].ranks()
+w = parity.assert_ranks_close(got, exp)
+print("ok worst %%.1e" %% w)
+'''
+cases = int(sys.argv[1]) if len(sys.argv) > 1 else 60
+rng = random.Random(2026)
+for c in range(cases):
+    scale, ef = rng.randint(8, 17), rng.choice([1, 2, 4, 8, 16, 32])
+    seed, p, T = rng.randint(1, 10 ** 6), rng.choice([1, 1, 2, 3, 4]), rng.randint(1, 12)
+    env = dict(os.environ)
+    if rng.random() < 0.6:  # tiny stream geometry: every code path at small scale
+        env.update(PR_HOTLDS=str(rng.choice([64, 256, 1024, 4096])), PR_NLDS=str(rng.randint(0, 20)),
+                   PR_QH=str(rng.choice([256, 1024, 8192])), PR_SEG=str(rng.choice([128, 512, 4096])))
+    geo = " ".join(f"{k}={env[k]}" for k in ("PR_HOTLDS", "PR_NLDS", "PR_QH", "PR_SEG") if k in env)
+    src = CASE % dict(root=ROOT, scale=scale, ef=ef, seed=seed, p=p, T=T)
+    r = subprocess.run([sys.executable, "-c", src], env=env, capture_output=True, text=True, timeout=300)
+    tag = f"case {c}: scale {scale} ef {ef} seed {seed} p {p} T {T} {geo}"
+    if r.returncode != 0:
+        print(tag, "FAILED\n", r.stdout[-2000:], r.stderr[-4000:])
+        sys.exit(1)
+    print(tag, r.stdout.strip(), flush=True)
