@@ -55,6 +55,9 @@ struct IterState {
 
 struct Tuning {
   uint32_t qh = 458752; // PR_QH: L2-hot segment length per slice after the LDS blocks (3.5 MiB)
+  uint32_t rb = 1024;   // PR_RB: rows per row-launch block (64..1024)
+  uint32_t rb_heavy = 256;  // PR_RBH: rows per heavy row-launch block
+  uint32_t heavy_deg = 128; // PR_HDEG: rows with in-degree >= this get heavy blocks (0 = none)
   int nlds = 18;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
   // PR_NT: 2 = non-temporal piece stores (they stop evicting x from the L2s: +3 %), 0 =
@@ -129,6 +132,8 @@ struct DevGraph {
   IterState* state = nullptr;
   // row launch: blocks of 1024 rows (class A, then class B), streams = slices x segments
   uint32_t nb_rows = 0, nb_rows_a = 0, n_streams = 0;
+  uint32_t row_rb = 1024;          // rows per row-launch block
+  uint32_t row_nbH = 0, row_rbH = 256, row_lH = 0;  // heavy row blocks (first lH rows)
   Tuning tune;
 };
 

@@ -175,6 +175,8 @@ struct RowArgs {
   const double* partial;   // per-piece partial sums of this round
   const uint16_t* roff;    // per-piece row offset inside its block
   uint32_t NS, nbA, lA, lrows;
+  uint32_t rb;             // rows per block (<= RB)
+  uint32_t nbH, rbH, lH;   // heavy blocks: the first lH class-A rows in nbH blocks of rbH rows
   const uint32_t* meta;
   double* x_out;           // this rank's slot of the next x
   const double* r_old;     // tracked mode: previous ranks (nullptr = r^0 == 1)
@@ -256,8 +258,12 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   for (int i = tid; i < 4 * REC_WORDS; i += BLOCK) (&lds[0][0])[i] = 0;
   // the block's rows; their epilogue inputs are loaded now, used after the piece loop
   const bool clsB = b >= A.nbA;
-  const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * RB : b * RB;
-  const uint32_t rb1 = min(rb0 + RB, clsB ? A.lrows : A.lA);
+  // the highest in-degree rows (one piece per stream each) come first in smaller blocks, so
+  // no single block's piece loop outlasts the launch when a rank holds few blocks
+  const bool heavy = b < A.nbH;
+  const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * A.rb
+                            : (heavy ? b * A.rbH : A.lH + (b - A.nbH) * A.rb);
+  const uint32_t rb1 = min(rb0 + (heavy ? A.rbH : A.rb), clsB ? A.lrows : A.lA);
   constexpr int RPT = RB / BLOCK;  // rows per thread
   uint32_t mt[RPT];
   double ro[RPT];
@@ -1157,13 +1163,25 @@ __global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, uint3
 
 // row blocks of the row launch: class-A rows in blocks of RB, then class-B rows
 struct RowBlocks {
-  uint32_t lA, nbA, NB, NS;
+  uint32_t lA, nbA, NB, NS, rb;
+  uint32_t nbH, rbH, lH;  // heavy blocks first: rows [0, lH) in blocks of rbH
 };
 __device__ __forceinline__ uint32_t block_of_row(const RowBlocks& B, uint32_t l) {
-  return l < B.lA ? l / RB : B.nbA + (l - B.lA) / RB;
+  if (l < B.lH) return l / B.rbH;
+  return l < B.lA ? B.nbH + (l - B.lH) / B.rb : B.nbA + (l - B.lA) / B.rb;
 }
 __device__ __forceinline__ uint32_t block_row0(const RowBlocks& B, uint32_t b) {
-  return b < B.nbA ? b * RB : B.lA + (b - B.nbA) * RB;
+  if (b < B.nbH) return b * B.rbH;
+  return b < B.nbA ? B.lH + (b - B.nbH) * B.rb : B.lA + (b - B.nbA) * B.rb;
+}
+
+// local class-A rows with in-degree >= thr (a prefix: rows are in-degree sorted)
+__global__ void k_count_heavy(const uint32_t* perm, const uint32_t* indeg, uint32_t lA, Layout L,
+                              uint32_t thr, unsigned* cnt) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool h = l < lA && indeg[perm[row_of(L, l)]] >= thr;
+  const uint64_t m = __ballot(h);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(cnt, static_cast<unsigned>(__popcll(m)));
 }
 
 // per-piece row offset in its block + run starts T[block][stream] (sentinel where empty)
@@ -1399,6 +1417,9 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.nt = env_int("PR_NT", T.nt);
   T.hot_lds = static_cast<uint32_t>(std::max(0, std::min(20480, env_int("PR_HOTLDS", static_cast<int>(T.hot_lds)))));
   T.dbg = env_int("PR_DBG", 0);
+  T.rb_heavy = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RBH", static_cast<int>(T.rb_heavy)))));
+  T.heavy_deg = static_cast<uint32_t>(std::max(0, env_int("PR_HDEG", static_cast<int>(T.heavy_deg))));
+  T.rb = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RB", static_cast<int>(T.rb)))));
   T.nlds = std::max(0, std::min(64, env_int("PR_NLDS", T.nlds)));
   T.stream_wg = std::max(1, std::min(2, env_int("PR_STREAM_WG", T.stream_wg)));
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
@@ -1689,9 +1710,29 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   const uint64_t NP = g->n_pieces;
   // ---- row launch: row blocks, per-piece row offsets, run table ------------------------------
   RowBlocks RBk{};
+  const uint32_t rbs = T.rb;
   RBk.lA = g->lA;
-  RBk.nbA = (g->lA + RB - 1) / RB;
-  RBk.NB = RBk.nbA + (lrows - g->lA + RB - 1) / RB;
+  RBk.rb = rbs;
+  RBk.rbH = std::min(T.rb_heavy, rbs);
+  RBk.nbH = RBk.lH = 0;
+  if (T.heavy_deg && g->lA) {
+    unsigned* hc = nullptr;
+    TRY(dmalloc(&hc, 1, err));
+    HIPTRY(hipMemsetAsync(hc, 0, 4, s));
+    hipLaunchKernelGGL(k_count_heavy, dim3(grid_for(g->lA)), dim3(BLOCK), 0, s, g->perm, g->indeg, g->lA, L, T.heavy_deg, hc);
+    unsigned nh = 0;
+    HIPTRY(hipMemcpyAsync(&nh, hc, 4, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(hc);
+    RBk.nbH = (nh + RBk.rbH - 1) / RBk.rbH;
+    RBk.lH = std::min(RBk.nbH * RBk.rbH, g->lA);
+  }
+  RBk.nbA = RBk.nbH + (g->lA - RBk.lH + rbs - 1) / rbs;
+  RBk.NB = RBk.nbA + (lrows - g->lA + rbs - 1) / rbs;
+  g->row_rb = rbs;
+  g->row_nbH = RBk.nbH;
+  g->row_rbH = RBk.rbH;
+  g->row_lH = RBk.lH;
   RBk.NS = NSLICE * g->nseg;
   if (RBk.NS > static_cast<uint32_t>(MAX_NS)) {
     if (err) *err = "too many stream segments for the row launch (raise PR_SEG)";
@@ -1829,6 +1870,10 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.roff = g->roff;
   A.dbg = static_cast<uint32_t>(g->tune.dbg);
   A.NS = g->n_streams;
+  A.rb = g->row_rb;
+  A.nbH = g->row_nbH;
+  A.rbH = g->row_rbH;
+  A.lH = g->row_lH;
   A.nbA = g->nb_rows_a;
   A.lA = g->lA;
   A.lrows = g->lrows;
@@ -2019,7 +2064,8 @@ int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s,
   TRY(dmalloc(&k1, m, err)); fr.v.push_back(k1);
   TRY(dmalloc(&rp, g->lrows + 1ull, err)); fr.v.push_back(rp);
   TRY(dmalloc(&c, m, err)); fr.v.push_back(c);
-  const RowBlocks RBk{g->lA, g->nb_rows_a, g->nb_rows, g->n_streams};
+  const RowBlocks RBk{g->lA, g->nb_rows_a, g->nb_rows, g->n_streams, g->row_rb,
+                      g->row_nbH, g->row_rbH, g->row_lH};
   if (g->nb_rows) hipLaunchKernelGGL(k_piece_row_runs, dim3(grid_loop(static_cast<uint64_t>(g->nb_rows) * g->n_streams)), dim3(BLOCK), 0, s, g->runs, g->roff, RBk, prow);
   if (g->stream_len) hipLaunchKernelGGL(k_export_keys, dim3(grid_loop(g->stream_len)), dim3(BLOCK), 0, s, g->col, g->col16, reinterpret_cast<const uint32_t*>(g->bits), g->task_piece, prow, L, g->d_gstart, g->d_gtask, g->d_gbase, static_cast<uint32_t>(g->gtask.size() - 1), g->nlds, g->hot_h, g->stream_len, k0);
   rocprim::double_buffer<uint64_t> db(k0, k1);

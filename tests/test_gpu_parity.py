@@ -313,6 +313,30 @@ def test_stream_layout_tiny_blocks(P, O, tiny_blocks, scale, ef, seed):
         grp.close()
 
 
+@pytest.mark.parametrize("hdeg,rbh", [(3, 64), (40, 256), (1, 1024)])
+def test_heavy_row_blocks(P, O, monkeypatch, hdeg, rbh):
+    """The highest in-degree rows go to smaller row-launch blocks (PR_HDEG / PR_RBH): ranks
+    match the oracle for p = 1 and a 3-rank group, and the exported CSR is the same graph."""
+    monkeypatch.setenv("PR_HDEG", str(hdeg))
+    monkeypatch.setenv("PR_RBH", str(rbh))
+    g = O.Graph.from_rmat(15, 16, 9)
+    exp = g.run(10)["ranks"]
+    eng = P.Engine()
+    eng.generate_rmat(15, 16, 9)
+    eng.run(10)
+    parity.assert_ranks_close(eng.ranks(), exp)
+    rp, col, od, dw = eng.export_csr()
+    indeg = np.diff(rp.astype(np.int64))
+    assert np.all(indeg >= 0) and int(rp[-1]) == len(col) == eng.info()["nnz"]
+    assert np.array_equal(np.sort(indeg), np.sort(g.degrees()[1].astype(np.int64)))
+    eng.close()
+    grp = P.LocalGroup(3)
+    grp.each("generate_rmat", 15, 16, 9)
+    grp.run(10)
+    parity.assert_ranks_close(grp.members[0].ranks(), exp)
+    grp.close()
+
+
 def test_export_csr_is_the_same_graph(P, O):
     """pr_export_csr rebuilds the pull CSR from the streams (internal ids): the oracle run on
     it gives the engine's rank multiset, and its degrees match the edge set."""
