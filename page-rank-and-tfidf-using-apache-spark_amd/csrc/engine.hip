@@ -1420,7 +1420,11 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.rb_heavy = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RBH", static_cast<int>(T.rb_heavy)))));
   T.heavy_deg = static_cast<uint32_t>(std::max(0, env_int("PR_HDEG", static_cast<int>(T.heavy_deg))));
   T.rb = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RB", static_cast<int>(T.rb)))));
-  T.nlds = std::max(0, std::min(64, env_int("PR_NLDS", T.nlds)));
+  // a rank's share of each (slice, LDS block) phase shrinks with p while the per-phase cost
+  // (block fill, phase tail) stays: fewer blocks per slice at p > 1 (measured per-rank SpMV
+  // at scale 26: p = 2 best at 15, p = 4 and 8 at 12; profiles/r01/multirank/)
+  const int nlds_def = p >= 4 ? 12 : (p >= 2 ? 15 : T.nlds);
+  T.nlds = std::max(0, std::min(64, env_int("PR_NLDS", nlds_def)));
   T.stream_wg = std::max(1, std::min(2, env_int("PR_STREAM_WG", T.stream_wg)));
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   const uint32_t n = in.n;
