@@ -1412,7 +1412,9 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   const int p = g->p, rank = g->rank;
   dev_free(g);
   Tuning& T = g->tune;
-  T.qh = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_QH", static_cast<int>(T.qh))));
+  // p >= 4: a 1.5 MiB L2-hot range (per-rank SpMV -2 % at p = 8, -3 % at p = 4)
+  const int qh_def = p >= 4 ? 196608 : static_cast<int>(T.qh);
+  T.qh = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_QH", qh_def)));
   T.seg = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_SEG", static_cast<int>(T.seg))));
   T.nt = env_int("PR_NT", T.nt);
   T.hot_lds = static_cast<uint32_t>(std::max(0, std::min(20480, env_int("PR_HOTLDS", static_cast<int>(T.hot_lds)))));
