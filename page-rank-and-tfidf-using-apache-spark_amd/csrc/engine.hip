@@ -1412,8 +1412,8 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   const int p = g->p, rank = g->rank;
   dev_free(g);
   Tuning& T = g->tune;
-  // p >= 4: a 1.5 MiB L2-hot range (per-rank SpMV -2 % at p = 8, -3 % at p = 4)
-  const int qh_def = p >= 4 ? 196608 : static_cast<int>(T.qh);
+  // p >= 2: a 1.5 MiB L2-hot range (per-rank SpMV -3 % at p = 2 and 4, -2 % at p = 8)
+  const int qh_def = p >= 2 ? 196608 : static_cast<int>(T.qh);
   T.qh = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_QH", qh_def)));
   T.seg = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_SEG", static_cast<int>(T.seg))));
   T.nt = env_int("PR_NT", T.nt);
