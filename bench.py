@@ -125,9 +125,14 @@ def main():
     gteps = nnz / (ms_step * 1e-3) / 1e9
     workload = f"rmat-s{a.scale}-ef{a.edge_factor}"
     # roofline of the SpMV of one round (stream launch + row launch, bracketed by HIP events on
-    # the engine stream): SURVEY.md 8d algorithmic bytes, this rank's share
+    # the engine stream): SURVEY.md 8d algorithmic bytes per launch.  p = 1: 4 nnz + 24 N + 8.
+    # p > 1, per rank: its own edges' columns, the WHOLE x (every rank gathers from all
+    # sources), its share of row pointers and rank writes: 4 local_nnz + 8 N + 16 N / p + 8.
     local_nnz = int(info["local_nnz"])
-    bytes_launch = 4 * local_nnz + 24 * n // world + 8
+    if world == 1:
+        bytes_launch = 4 * local_nnz + 24 * n + 8
+    else:
+        bytes_launch = 4 * local_nnz + 8 * n + 16 * n // world + 8
     kms = st["ms_spmv_kernel"]
     achieved = bytes_launch / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = load_traffic(a.traffic_json, f"{workload}-p{world}")
@@ -157,11 +162,15 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "kernel": "spmv_stream+spmv_rows (the SpMV of one round)",
+                         "time_source": "HIP events on the engine stream around the two "
+                                        "launches of each round, mean over the timed rounds "
+                                        "(pr_stats.ms_spmv_kernel)",
                          "kernel_ms": round(kms, 4),
                          "algorithmic_bytes_per_launch": bytes_launch},
             "cpu_baseline": cpu,
             "device_ms_per_round": round(st["ms_per_iter"], 4),
             "build_s": round(build_s, 2),
+            "build_id": P.build_id(),
         }
         print(json.dumps(line), flush=True)
     eng.close()

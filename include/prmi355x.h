@@ -99,11 +99,17 @@ typedef struct {
   uint64_t local_nnz;     /* edges owned by this rank                                     */
   double ms_ingest;       /* host parse + hashing                                         */
   double ms_build;        /* device CSR build                                             */
-  uint64_t reserved[6];
+  uint64_t ingest_flags;  /* bit 0: the text was parsed on the host because it does not fit
+                             the device ingest (>= 2^30 id tokens or device memory)         */
+  uint64_t reserved[5];
 } pr_graph_info;
 
 /* Library version "major.minor". */
 const char* pr_version(void);
+/* Identity of the sources the library was compiled from (hash of csrc/, include/ and the
+ * Makefile, page-rank-and-tfidf-using-apache-spark_amd/source_hash.py).  The tests compare it
+ * with the checked-out tree, so a stale binary is never tested as HEAD. */
+const char* pr_build_id(void);
 void pr_opts_default(pr_opts* opts);
 
 /* SparkConf + JavaSparkContext (PageRank.java:22-23): binds the device / rank. */
@@ -178,6 +184,13 @@ int pr_topk(pr_ctx* ctx, uint32_t k, uint64_t* pair_out, uint32_t* id_out, doubl
 /* FileWriter("./topPage") loop (PageRank.java:190-204): `title \t Double.toString(rank)`
  * for the top opts.topk rows.  Only rank 0 writes.  Collective. */
 int pr_write_top_page(pr_ctx* ctx, const char* path);
+
+/* Full rank dump (extends the output contract of PageRank.java:167-204):
+ * every page of the final ranks RDD, in vertex-id order (first appearance in the input), one
+ * line per mapping pair of the page -- `id \t title \t Double.toString(rank)` -- i.e. the
+ * rows of ranks.join(mappings) (:168) without sortByKey/take; a ranked page with no title
+ * gets one line with an empty title.  Only rank 0 writes.  Collective. */
+int pr_write_rank_dump(pr_ctx* ctx, const char* path);
 
 /* Id / title strings (the reference's String keys).  *len = full length; at most cap
  * bytes copied.  For generated / in-memory graphs the id string is the decimal id. */

@@ -45,6 +45,7 @@ struct pr_ctx {
   std::vector<pr_ctx*> group;    // single-process rank group (pr_comm_init_local)
   int seed_rounds = 0;           // pr_set_ranks: rounds behind the seed (0 = no seed)
   prmi::TfidfState tf;           // the TF-IDF job (Spark.java)
+  bool ingest_fallback = false;  // last text ingest went to the host parser (too large)
 };
 
 namespace {
@@ -477,7 +478,12 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
     if (st) *st = s;
     return PR_OK;
   }
-  if (c0->dg.W0 == 0) {
+  // every member seeded alike (pr_set_ranks / pr_checkpoint_load on each), as pr_run
+  for (int i = 1; i < n; ++i)
+    if (ctxs[i]->dg.seeded != c0->dg.seeded || ctxs[i]->seed_rounds != c0->seed_rounds)
+      return fail(c0, PR_E_ARG, "local group: members seeded differently (call set_ranks on every member)");
+  const int r0 = c0->dg.seeded ? c0->seed_rounds : 0;  // rounds behind the starting ranks
+  if (!c0->dg.seeded && c0->dg.W0 == 0) {  // round 1 reduces an empty danglingMap (:125)
     s.failed_iteration = 1;
     if (st) *st = s;
     return fail(c0, PR_E_EMPTY_DANGLING, "java.lang.UnsupportedOperationException: empty collection (iteration 1)");
@@ -538,11 +544,11 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
   s.residual = tracked ? hs.resid : 0.0;
   s.rank_sum = tracked ? hs.rank_sum : 0.0;
   if (hs.err_iter != 0 && hs.err_iter <= done) {
-    s.failed_iteration = hs.err_iter;
+    s.failed_iteration = r0 + hs.err_iter;
     if (st) *st = s;
     return fail(c0, PR_E_EMPTY_DANGLING,
                 "java.lang.UnsupportedOperationException: empty collection (iteration " +
-                    std::to_string(hs.err_iter) + ")");
+                    std::to_string(r0 + hs.err_iter) + ")");
   }
   finish(done);
   if (st) *st = s;
@@ -556,14 +562,24 @@ int pr_ingest_buffers(pr_ctx* c, const char* arcs, size_t alen, const char* map,
   auto t0 = std::chrono::steady_clock::now();
   c->hg = HostGraph();
   c->have_graph = false;
+  c->ingest_fallback = false;
   prmi::ParseError pe;
   bool parsed = true;
   if (c->has_device) {  // device ingest (ingest.hip); host parser for host-only contexts
     std::string err;
     HIPCHK(c, hipSetDevice(c->device));
     rc = prmi::dev_ingest_text(arcs ? arcs : "", alen, map ? map : "", mlen, &c->hg, &pe, c->stream, &err);
-    if (rc == PR_E_PARSE) parsed = false;
-    else if (rc) {
+    if (rc == prmi::INGEST_NOFIT || rc == PR_E_OOM) {
+      // too large for the device tables / line index: the host parser has no such limit
+      if ((c->opts.flags & PR_F_VERBOSE) || getenv("PR_VERBOSE"))
+        fprintf(stderr, "[prmi355x] device ingest: %s; parsing on the host\n", err.c_str());
+      (void)hipGetLastError();
+      c->hg = HostGraph();
+      parsed = prmi::ingest_text(arcs ? arcs : "", alen, map ? map : "", mlen, &c->hg, &pe);
+      c->ingest_fallback = true;
+    } else if (rc == PR_E_PARSE) {
+      parsed = false;
+    } else if (rc) {
       c->hg = HostGraph();
       return fail(c, rc, "device ingest: " + err);
     }
@@ -674,6 +690,7 @@ int pr_graph_get_info(pr_ctx* c, pr_graph_info* o) {
   o->n_tot = c->hg.n_tot;
   o->n_pairs = pair_count(c);
   o->ms_ingest = c->ms_ingest;
+  o->ingest_flags = c->ingest_fallback ? 1u : 0u;
   if (c->has_device) {
     o->nnz = c->dg.nnz;
     o->dangling_entries = c->dg.n_dang_entries;
@@ -827,6 +844,65 @@ int pr_write_top_page(pr_ctx* c, const char* path) {
   const int cl = fclose(f);
   if (w != out.size() || cl != 0) return fail(c, PR_E_IO, "java.io.IOException: short write");
   return PR_OK;
+}
+
+int pr_write_rank_dump(pr_ctx* c, const char* path) {
+  if (!c || !path) return c ? fail(c, PR_E_ARG, "null path") : PR_E_ARG;
+  int rc = gather_ranks(c);  // collective
+  if (rc) return rc;
+  if (c->opts.rank != 0) return PR_OK;
+  FILE* f = fopen(path, "wb");
+  if (!f) return fail(c, PR_E_IO, std::string("java.io.IOException: cannot open ") + path);
+  const PairIndex pi = make_pair_index(c);
+  const bool text = c->source == pr_ctx::SRC_TEXT;
+  if (text) ensure_pairs_by_id(c);
+  std::string out;
+  out.reserve(1 << 22);
+  char num[64];
+  bool ok = true;
+  for (uint32_t v = 0; v < c->hg.n && ok; ++v) {
+    const double r = c->h_ranks[v];
+    if (!(r > 0.0)) continue;  // not in the ranks RDD
+    prmi::java_double_to_string(r, num, sizeof(num));
+    std::string id;
+    if (text) {
+      size_t n;
+      const char* p = c->hg.ids.get(v, &n);
+      id.assign(p, n);
+    } else {
+      id = std::to_string(v);
+    }
+    uint64_t b = v, e = v + 1ull;  // the mapping pairs of page v (:167 join)
+    if (text) {
+      b = c->hg.pair_first[v];
+      e = c->hg.pair_first[v + 1];
+    } else if (!c->hg.mapw.empty()) {
+      b = pi.first[v];
+      e = pi.first[v + 1];
+    }
+    auto row = [&](const std::string& title) {
+      out += id;
+      out += '\t';
+      out += title;
+      out += '\t';
+      out += num;
+      out += '\n';
+    };
+    if (b == e) row("");  // a ranked page without a title (the join would drop it)
+    for (uint64_t q = b; q < e; ++q) {
+      uint32_t vv;
+      std::string t;
+      pair_at(c, pi, text ? c->hg.pairs_by_id[q] : q, &vv, &t);
+      row(t);
+    }
+    if (out.size() >= (1u << 22)) {
+      ok = fwrite(out.data(), 1, out.size(), f) == out.size();
+      out.clear();
+    }
+  }
+  if (ok && !out.empty()) ok = fwrite(out.data(), 1, out.size(), f) == out.size();
+  ok = (fclose(f) == 0) && ok;
+  return ok ? PR_OK : fail(c, PR_E_IO, "java.io.IOException: short write");
 }
 
 int pr_id_string(pr_ctx* c, uint32_t v, char* buf, size_t cap, size_t* len) {

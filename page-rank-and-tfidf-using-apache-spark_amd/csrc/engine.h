@@ -205,7 +205,9 @@ int tf_lookup(TfidfState* t, const char* word, size_t wlen, std::vector<uint32_t
               std::vector<uint32_t>* tfs, uint32_t* df, hipStream_t s, std::string* err);
 
 // Text ingest on the device (ingest.hip): same result as ingest_text (host_graph.cpp).
-// PR_E_PARSE with *pe filled on a malformed line.
+// PR_E_PARSE with *pe filled on a malformed line; INGEST_NOFIT (or PR_E_OOM) when the input
+// does not fit the device path -- the caller then parses on the host.
+constexpr int INGEST_NOFIT = 100;
 int dev_ingest_text(const char* arcs, size_t alen, const char* map, size_t mlen, HostGraph* g,
                     ParseError* pe, hipStream_t s, std::string* err);
 int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s, std::string* err);

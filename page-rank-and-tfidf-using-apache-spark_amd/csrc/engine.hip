@@ -812,8 +812,15 @@ __global__ void k_make_keys(const uint32_t* src, const uint32_t* dst, uint64_t m
   }
 }
 
+// Degrees and the edge-set digest of the distinct edges (sorted by dst, then src).
+// out-degree (PageRank.java:103-108 urlCount): one integer atomic per edge on its source.
+// in-degree: run lengths of dst in the sorted keys (no atomics): the first edge of a run
+// records its position, the last one its end; k_indeg_from_runs subtracts.
+// digest {sum, xor} of mix64(src<<32|dst): per-block partials into DIGEST_SHARDS shards
+// (single-address atomics from every block serialised this kernel at scale 26).
+constexpr int DIGEST_SHARDS = 4096;
 __global__ void k_degrees(const uint64_t* uk, uint64_t nnz, int nb, uint32_t* outdeg,
-                          uint32_t* indeg, unsigned long long* digest) {
+                          uint64_t* run_lo, uint64_t* run_hi, unsigned long long* digest) {
   __shared__ unsigned long long ssum[BLOCK / 64], sxor[BLOCK / 64];
   PRMI_BLOCK_LOOP(nnz) {
     const uint64_t e = blk_ * blockDim.x + threadIdx.x;
@@ -823,7 +830,8 @@ __global__ void k_degrees(const uint64_t* uk, uint64_t nnz, int nb, uint32_t* ou
       const uint32_t d = static_cast<uint32_t>(k >> nb);
       const uint32_t s = static_cast<uint32_t>(k & ((1ull << nb) - 1));
       atomicAdd(&outdeg[s], 1u);
-      atomicAdd(&indeg[d], 1u);
+      if (e == 0 || static_cast<uint32_t>(uk[e - 1] >> nb) != d) run_lo[d] = e;
+      if (e + 1 == nnz || static_cast<uint32_t>(uk[e + 1] >> nb) != d) run_hi[d] = e + 1;
       h = mix64((static_cast<uint64_t>(s) << 32) | d);
     }
     uint64_t hs = h, hx = h;
@@ -843,17 +851,25 @@ __global__ void k_degrees(const uint64_t* uk, uint64_t nnz, int nb, uint32_t* ou
         a += ssum[i];
         x ^= sxor[i];
       }
-      atomicAdd(&digest[0], a);
-      atomicXor(&digest[1], x);
+      const uint64_t sh = 2 * (blk_ % DIGEST_SHARDS);
+      atomicAdd(&digest[sh], a);
+      atomicXor(&digest[sh + 1], x);
     }
     __syncthreads();  // the next iteration reuses the shared partials
   }
 }
 
+__global__ void k_indeg_from_runs(const uint64_t* run_lo, const uint64_t* run_hi, uint32_t n,
+                                  uint32_t* indeg) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n) indeg[v] = static_cast<uint32_t>(run_hi[v] - run_lo[v]);
+}
+
 // dangling weight (PageRank.java:56) + class key for the vertex order
+constexpr int W_SHARDS = 64;
 __global__ void k_vertex_keys(const uint32_t* outdeg, const uint32_t* indeg, const uint32_t* mapw,
                               uint32_t n, uint32_t* dang_w, uint64_t* vkey, uint32_t* vid,
-                              unsigned long long* sums /* [0]=W0 [1]=dangling entries */) {
+                              unsigned long long* sums /* [W_SHARDS] shards of W0 */) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t w = 0;
   if (v < n) {
@@ -867,7 +883,9 @@ __global__ void k_vertex_keys(const uint32_t* outdeg, const uint32_t* indeg, con
   uint64_t s = w;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(&sums[0], static_cast<unsigned long long>(s));
+  // one shard per (block mod W_SHARDS): no single-address atomic from every wave
+  if ((threadIdx.x & 63) == 0 && s)
+    atomicAdd(&sums[blockIdx.x % W_SHARDS], static_cast<unsigned long long>(s));
 }
 
 __global__ void k_class_count(const uint64_t* vkey_sorted, uint32_t n, unsigned* cnt) {
@@ -1030,38 +1048,27 @@ __device__ __forceinline__ uint32_t col_of_xpos(const Layout& L, uint32_t x) {
   return L.R + ((rem / CHUNK) * NSLICE + sl) * CHUNK + rem % CHUNK;
 }
 
-// relabel unique edges to stream keys (slice, segment, local row, q within segment) and keep
-// this rank's rows (wave-aggregated append when p > 1)
+// relabel unique edges to stream keys (slice, segment, local row, q within segment); with p > 1
+// the edges of other ranks' rows get DROP_KEY and a rocprim::select keeps this rank's
+constexpr uint64_t DROP_KEY = ~0ull;
+struct NotDropped {
+  __device__ __host__ bool operator()(uint64_t k) const { return k != DROP_KEY; }
+};
 __global__ void k_stream_keys(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv,
-                              Layout L, StreamGeo G, unsigned long long* counter, uint64_t* out) {
+                              Layout L, StreamGeo G, uint64_t* out) {
   PRMI_BLOCK_LOOP(nnz) {
     const uint64_t e = blk_ * blockDim.x + threadIdx.x;
-    bool keep = false;
-    uint64_t key = 0;
-    if (e < nnz) {
-      const uint64_t k = uk[e];
-      const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
-      const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
-      keep = owner_of(L, kd) == L.rank;
-      uint32_t sl, q, seg, qin;
-      col_slice_q(L, G, ks, sl, q);
-      seg_of_q(G, q, seg, qin);
-      key = (static_cast<uint64_t>(sl) << (G.sgb + G.rb + G.qb)) |
-            (static_cast<uint64_t>(seg) << (G.rb + G.qb)) |
-            (static_cast<uint64_t>(local_of(L, kd)) << G.qb) | qin;
-    }
-    if (L.p == 1) {
-      if (e < nnz) out[e] = key;
-      continue;
-    }
-    const uint64_t mask = __ballot(keep);
-    if (!mask) continue;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(counter, static_cast<unsigned long long>(__popcll(mask)));
-    base = __shfl(base, leader);
-    if (keep) out[base + __popcll(mask & ((1ull << lane) - 1))] = key;
+    if (e >= nnz) continue;
+    const uint64_t k = uk[e];
+    const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
+    const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
+    uint32_t sl, q, seg, qin;
+    col_slice_q(L, G, ks, sl, q);
+    seg_of_q(G, q, seg, qin);
+    const uint64_t key = (static_cast<uint64_t>(sl) << (G.sgb + G.rb + G.qb)) |
+                         (static_cast<uint64_t>(seg) << (G.rb + G.qb)) |
+                         (static_cast<uint64_t>(local_of(L, kd)) << G.qb) | qin;
+    out[e] = owner_of(L, kd) == L.rank ? key : DROP_KEY;
   }
 }
 
@@ -1078,29 +1085,55 @@ __global__ void k_group_starts(const uint64_t* key, uint64_t n, StreamGeo G,
 }
 
 // column of every stream edge (LDS groups: u16 offset inside the block; L2 group: x position)
-// + the pair-start flags (indexed by global stream position = task * TASK + offset)
 __global__ void k_stream_fill(const uint64_t* key, uint64_t n, Layout L, StreamGeo G,
-                              const uint64_t* gstart, const uint32_t* gtask,
-                              const uint64_t* gbase, uint32_t* col, uint16_t* col16,
-                              uint32_t* bits32, unsigned long long* n_pairs) {
+                              const uint64_t* gstart, const uint64_t* gbase, uint32_t* col,
+                              uint16_t* col16) {
   PRMI_BLOCK_LOOP(n) {
     const uint64_t e = blk_ * blockDim.x + threadIdx.x;
-    bool start = false;
-    if (e < n) {
-      const uint64_t k = key[e];
-      const uint32_t gr = group_of_key(G, k);
-      const uint64_t rel = e - gstart[gr];
-      const uint64_t pos = static_cast<uint64_t>(gtask[gr]) * TASK + rel;
-      const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
-      const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
-      const uint32_t qin = static_cast<uint32_t>(k & ((1ull << G.qb) - 1));
-      if (seg < G.nlds) col16[gbase[gr] + rel] = static_cast<uint16_t>(qin);
-      else col[gbase[gr] + rel] = xpos(L, col_of_slice_q(L, G, sl, q_of_seg(G, seg, qin)));
-      start = e == gstart[gr] || (key[e - 1] >> G.qb) != (k >> G.qb);
-      if (start) atomicOr(&bits32[pos / 32], 1u << (pos % 32));
+    if (e >= n) continue;
+    const uint64_t k = key[e];
+    const uint32_t gr = group_of_key(G, k);
+    const uint64_t rel = e - gstart[gr];
+    const uint32_t sl = static_cast<uint32_t>(k >> (G.sgb + G.rb + G.qb));
+    const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
+    const uint32_t qin = static_cast<uint32_t>(k & ((1ull << G.qb) - 1));
+    if (seg < G.nlds) col16[gbase[gr] + rel] = static_cast<uint16_t>(qin);
+    else col[gbase[gr] + rel] = xpos(L, col_of_slice_q(L, G, sl, q_of_seg(G, seg, qin)));
+  }
+}
+
+// pair-start flags, one 32-bit word per thread (indexed by stream position = task * TASK +
+// offset; groups start on task boundaries, so a word never spans two groups): bit b is set
+// when edge pos0 + b starts a (row, slice, segment) pair.  No atomics on the words; the pair
+// count goes to NPAIR_SHARDS shards.
+constexpr int NPAIR_SHARDS = 1024;
+__global__ void k_stream_bits(const uint64_t* key, const uint64_t* gstart, const uint32_t* gtask,
+                              uint32_t ngroups, uint64_t nwords, int qb, uint32_t* bits32,
+                              unsigned long long* npair) {
+  PRMI_BLOCK_LOOP(nwords) {
+    const uint64_t w = blk_ * blockDim.x + threadIdx.x;
+    uint32_t word = 0;
+    if (w < nwords) {
+      const uint64_t pos0 = w * 32;
+      const uint64_t t = pos0 / TASK;
+      uint32_t lo = 0, hi = ngroups - 1;  // last group whose first task <= t
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if (gtask[mid] <= t) lo = mid; else hi = mid - 1;
+      }
+      const uint64_t rel0 = pos0 - static_cast<uint64_t>(gtask[lo]) * TASK;
+      const uint64_t g0 = gstart[lo], glen = gstart[lo + 1] - g0;
+      uint64_t prev = rel0 ? key[g0 + rel0 - 1] >> qb : ~0ull;
+      for (int b = 0; b < 32 && rel0 + b < glen; ++b) {
+        const uint64_t cur = key[g0 + rel0 + b] >> qb;
+        if (cur != prev) word |= 1u << b;
+        prev = cur;
+      }
+      bits32[w] = word;
     }
-    const uint64_t s = wave_sum_u64(start ? 1u : 0u);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(n_pairs, static_cast<unsigned long long>(s));
+    const uint64_t c = wave_sum_u64(__popc(word));
+    if ((threadIdx.x & 63) == 0 && c)
+      atomicAdd(&npair[blk_ % NPAIR_SHARDS], static_cast<unsigned long long>(c));
   }
 }
 
@@ -1506,12 +1539,41 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&g->indeg, n, err));
   TRY(dmalloc(&g->dang_w, n, err));
   TRY(dmalloc(&g->perm, n, err));
-  unsigned long long* d_sums = nullptr;  // [0,2) digest, [2] W0
-  TRY(dmalloc(&d_sums, 4, err));
-  HIPTRY(hipMemsetAsync(d_sums, 0, 32, s));
+  unsigned long long* d_sums = nullptr;  // shards of W0
+  unsigned long long* d_dig = nullptr;   // digest shards
+  TRY(dmalloc(&d_sums, W_SHARDS, err));
+  TRY(dmalloc(&d_dig, 2 * DIGEST_SHARDS, err));
+  HIPTRY(hipMemsetAsync(d_sums, 0, 8ull * W_SHARDS, s));
+  HIPTRY(hipMemsetAsync(d_dig, 0, 16ull * DIGEST_SHARDS, s));
   HIPTRY(hipMemsetAsync(g->outdeg, 0, 4ull * (n ? n : 1), s));
-  HIPTRY(hipMemsetAsync(g->indeg, 0, 4ull * (n ? n : 1), s));
-  if (nnz) hipLaunchKernelGGL(k_degrees, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, g->outdeg, g->indeg, d_sums);
+  {
+    uint64_t *run_lo = nullptr, *run_hi = nullptr;  // per dst: [first, one past last) edge
+    TRY(dmalloc(&run_lo, n, err));
+    if (dmalloc(&run_hi, n, err) != PR_OK) {
+      (void)hipFree(run_lo);
+      return PR_E_OOM;
+    }
+    HIPTRY(hipMemsetAsync(run_lo, 0, 8ull * (n ? n : 1), s));
+    HIPTRY(hipMemsetAsync(run_hi, 0, 8ull * (n ? n : 1), s));
+    if (nnz) hipLaunchKernelGGL(k_degrees, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, g->outdeg, run_lo, run_hi, d_dig);
+    if (n) hipLaunchKernelGGL(k_indeg_from_runs, dim3(grid_for(n)), dim3(BLOCK), 0, s, run_lo, run_hi, n, g->indeg);
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(run_lo);
+    (void)hipFree(run_hi);
+  }
+  {
+    std::vector<unsigned long long> dig(2 * DIGEST_SHARDS);
+    HIPTRY(hipMemcpyAsync(dig.data(), d_dig, 16ull * DIGEST_SHARDS, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(d_dig);
+    unsigned long long a = 0, x = 0;
+    for (int i = 0; i < DIGEST_SHARDS; ++i) {
+      a += dig[2 * i];
+      x ^= dig[2 * i + 1];
+    }
+    g->digest[0] = a;
+    g->digest[1] = x;
+  }
   uint32_t* d_mapw = nullptr;
   if (in.h_mapw) {
     TRY(dmalloc(&d_mapw, n, err));
@@ -1522,7 +1584,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&vk, n, err));
   TRY(dmalloc(&vk2, n, err));
   TRY(dmalloc(&vid, n, err));
-  if (n) hipLaunchKernelGGL(k_vertex_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->outdeg, g->indeg, d_mapw, n, g->dang_w, vk, vid, d_sums + 2);
+  if (n) hipLaunchKernelGGL(k_vertex_keys, dim3(grid_for(n)), dim3(BLOCK), 0, s, g->outdeg, g->indeg, d_mapw, n, g->dang_w, vk, vid, d_sums);
   HIPTRY(hipGetLastError());
   {
     size_t tb = 0;
@@ -1535,19 +1597,19 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   unsigned cls_first[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   HIPTRY(hipMemcpyAsync(d_cls, cls_first, 16, hipMemcpyHostToDevice, s));
   if (n) hipLaunchKernelGGL(k_class_count, dim3(grid_for(n)), dim3(BLOCK), 0, s, vk2, n, d_cls);
-  unsigned long long sums[4];
+  unsigned long long sums[W_SHARDS];
   HIPTRY(hipMemcpyAsync(cls_first, d_cls, 16, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(sums, d_sums, 32, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(sums, d_sums, 8ull * W_SHARDS, hipMemcpyDeviceToHost, s));
   HIPTRY(hipStreamSynchronize(s));
   (void)hipFree(d_cls);
   (void)hipFree(d_sums);
   (void)hipFree(vk);
   (void)hipFree(vk2);
   g->mapw = d_mapw;  // kept: the top-K selection weighs pages by their mapping pairs
-  g->digest[0] = sums[0];
-  g->digest[1] = sums[1];
-  g->W0 = sums[2];
-  g->n_dang_entries = sums[2];
+  uint64_t w0 = 0;
+  for (int i = 0; i < W_SHARDS; ++i) w0 += sums[i];
+  g->W0 = w0;
+  g->n_dang_entries = w0;
   uint32_t start[5];
   start[4] = n;
   for (int c = 3; c >= 0; --c) start[c] = cls_first[c] == 0xFFFFFFFFu ? start[c + 1] : cls_first[c];
@@ -1628,20 +1690,27 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
 
   // ---- local edges: stream keys, stable radix sort -------------------------------------------
   uint64_t* lk_in = uniq == kA ? kB : kA;  // free buffer
-  unsigned long long* d_cnt = nullptr;     // [0] local edges [1] pairs [2..] group starts
+  unsigned long long* d_cnt = nullptr;     // [0] local edges [1] unused [2..] group starts
   TRY(dmalloc(&d_cnt, 2 + NG, err));
   HIPTRY(hipMemsetAsync(d_cnt, 0, 16, s));
   HIPTRY(hipMemsetAsync(d_cnt + 2, 0xFF, 8ull * NG, s));
-  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, d_cnt, lk_in);
+  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, lk_in);
   uint64_t lnnz = nnz;
-  if (p > 1) {
+  uint64_t* lk_alt = uniq;  // the unique keys are dead from here: sort scratch
+  if (p > 1 && nnz) {  // keep this rank's rows' edges (order-preserving select)
+    size_t tb = 0;
+    HIPTRY(rocprim::select(nullptr, tb, lk_in, uniq, d_cnt, nnz, NotDropped(), s));
+    TRY(tmp.ensure(tb, err));
+    HIPTRY(rocprim::select(tmp.p, tb, lk_in, uniq, d_cnt, nnz, NotDropped(), s));
     HIPTRY(hipMemcpyAsync(&lnnz, d_cnt, 8, hipMemcpyDeviceToHost, s));
     HIPTRY(hipStreamSynchronize(s));
+    lk_alt = lk_in;
+    lk_in = uniq;
   }
   g->lnnz = lnnz;
   uint64_t* lk = nullptr;
   {
-    rocprim::double_buffer<uint64_t> db(lk_in, uniq);
+    rocprim::double_buffer<uint64_t> db(lk_in, lk_alt);
     size_t tb = 0;
     HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, lnnz, 0, key_bits, s));
     TRY(tmp.ensure(tb, err));
@@ -1694,7 +1763,11 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   if (g->n_col16) hipLaunchKernelGGL(k_fill_u16, dim3(grid_loop(g->n_col16)), dim3(BLOCK), 0, s, g->col16, g->n_col16, static_cast<uint16_t>(G.H));  // zero slot
   HIPTRY(hipMemsetAsync(g->bits, 0, 2 * (g->stream_len / EPL + 2), s));
   uint32_t* bits32 = reinterpret_cast<uint32_t*>(g->bits);
-  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_loop(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, g->d_gstart, g->d_gtask, g->d_gbase, g->col, g->col16, bits32, d_cnt + 1);
+  if (lnnz) hipLaunchKernelGGL(k_stream_fill, dim3(grid_loop(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, L, G, g->d_gstart, g->d_gbase, g->col, g->col16);
+  unsigned long long* d_npair = nullptr;
+  TRY(dmalloc(&d_npair, NPAIR_SHARDS, err));
+  HIPTRY(hipMemsetAsync(d_npair, 0, 8ull * NPAIR_SHARDS, s));
+  if (g->stream_len) hipLaunchKernelGGL(k_stream_bits, dim3(grid_loop(g->stream_len / 32)), dim3(BLOCK), 0, s, lk, g->d_gstart, g->d_gtask, NG, g->stream_len / 32, G.qb, bits32, d_npair);
   TRY(dmalloc(&g->task_piece, tasks + 1ull, err));
   {
     uint32_t* tcnt = nullptr;
@@ -1705,13 +1778,15 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     TRY(tmp.ensure(tb, err));
     HIPTRY(rocprim::exclusive_scan(tmp.p, tb, tcnt, g->task_piece, 0u, tasks + 1ull, rocprim::plus<uint32_t>(), s));
     uint32_t np = 0;
-    unsigned long long npairs = 0;
+    std::vector<unsigned long long> hp(NPAIR_SHARDS);
     HIPTRY(hipMemcpyAsync(&np, g->task_piece + tasks, 4, hipMemcpyDeviceToHost, s));
-    HIPTRY(hipMemcpyAsync(&npairs, d_cnt + 1, 8, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(hp.data(), d_npair, 8ull * NPAIR_SHARDS, hipMemcpyDeviceToHost, s));
     HIPTRY(hipStreamSynchronize(s));
     (void)hipFree(tcnt);
+    (void)hipFree(d_npair);
     g->n_pieces = np;
-    g->n_pairs = npairs;
+    g->n_pairs = 0;
+    for (unsigned long long v : hp) g->n_pairs += v;
   }
   const uint64_t NP = g->n_pieces;
   // ---- row launch: row blocks, per-piece row offsets, run table ------------------------------

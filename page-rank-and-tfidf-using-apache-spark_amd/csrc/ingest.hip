@@ -19,11 +19,14 @@
 //      (:43-51), and keyed by the whole line the distinct raw mapping lines N_tot (:60).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
 
+#include "engine.h"
 #include "host_graph.h"
 #include "text_device.h"
 
@@ -85,9 +88,13 @@ int dev_ingest_text(const char* arcs, size_t alen, const char* map, size_t mlen,
   const uint64_t La = line_count(0, alen, nEa, lastA);
   const uint64_t Lm = line_count(alen, nb, nEm, lastM);
   const uint64_t T64 = 2 * La + Lm;
-  if (T64 >= (1ull << 30)) {
-    if (err) *err = "input too large for the device ingest (>= 2^30 id tokens)";
-    return PR_E_ARG;
+  // 32-bit token indices in the id table; PR_INGEST_MAX_TOKENS lowers the cap (tests force
+  // the host fallback with it)
+  uint64_t cap = 1ull << 30;
+  if (const char* e = getenv("PR_INGEST_MAX_TOKENS")) cap = std::min<uint64_t>(cap, strtoull(e, nullptr, 0));
+  if (T64 >= cap) {
+    if (err) *err = "input too large for the device ingest (" + std::to_string(T64) + " id tokens)";
+    return prmi::INGEST_NOFIT;
   }
   const uint32_t T = static_cast<uint32_t>(T64);
   // split every line; id tokens: [2k] src, [2k+1] dst of arc line k, [2La + k] mapping id

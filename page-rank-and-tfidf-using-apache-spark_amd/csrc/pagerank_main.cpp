@@ -2,8 +2,10 @@
 // where no JVM is available.  Same job, same file contract, engine behind the C ABI.
 //
 //   pagerank [ARCS MAPPING [ITERATIONS]] [--out PATH] [--topk K] [--tol X] [--verbose]
-//            [--normalized] [--resume CKPT] [--checkpoint CKPT]
+//            [--normalized] [--resume CKPT] [--checkpoint CKPT] [--dump PATH]
 //
+// --dump writes every ranked page by id (`id \t title \t rank`, pr_write_rank_dump): the
+// full rank dump of SURVEY.md 8f #2 beside ./topPage.
 // --normalized, --resume and --checkpoint are not in the reference:
 // normalized ranks (r^0 = 1/N_tot, base 0.15/N_tot); continue from a checkpoint's ranks for
 // ITERATIONS more rounds; write the final ranks as a checkpoint.
@@ -30,7 +32,7 @@ static int die(pr_ctx* c, int rc) {
 
 int main(int argc, char** argv) {
   std::string arcs = "./wikipedia_arcs", mapping = "./wikipedia_mapping", out = "./topPage";
-  std::string resume, checkpoint;
+  std::string resume, checkpoint, dump;
   int iterations = 10, npos = 0;
   double tol = 0.0;
   pr_opts o;
@@ -44,9 +46,10 @@ int main(int argc, char** argv) {
     else if (a == "--normalized") o.flags |= PR_F_NORMALIZED;
     else if (a == "--resume" && i + 1 < argc) resume = argv[++i];
     else if (a == "--checkpoint" && i + 1 < argc) checkpoint = argv[++i];
+    else if (a == "--dump" && i + 1 < argc) dump = argv[++i];
     else if (a == "-h" || a == "--help") {
       printf("usage: %s [ARCS MAPPING [ITERATIONS]] [--out PATH] [--topk K] [--tol X] [--verbose]\n"
-             "          [--normalized] [--resume CKPT] [--checkpoint CKPT]\n", argv[0]);
+             "          [--normalized] [--resume CKPT] [--checkpoint CKPT] [--dump PATH]\n", argv[0]);
       return 0;
     } else {
       if (npos == 0) arcs = a;
@@ -74,6 +77,10 @@ int main(int argc, char** argv) {
   if (o.flags & PR_F_VERBOSE)
     fprintf(stderr, "[prmi355x] %d rounds, %.3f ms/round, %.2f GTEPS, nnz=%llu\n", st.iterations,
             st.ms_per_iter, st.gteps, static_cast<unsigned long long>(st.nnz));
+  if (!dump.empty()) {
+    rc = pr_write_rank_dump(c, dump.c_str());
+    if (rc) return die(c, rc);
+  }
   rc = pr_write_top_page(c, out.c_str());
   if (rc == PR_E_IO) {
     fprintf(stderr, "%s\n", pr_last_error(c));  // e.printStackTrace(), job still succeeds

@@ -88,7 +88,7 @@ class GraphInfo(C.Structure):
                 ("dangling_entries", C.c_uint64), ("n_sources", C.c_uint64),
                 ("n_rows", C.c_uint64), ("local_rows", C.c_uint64), ("local_nnz", C.c_uint64),
                 ("ms_ingest", C.c_double), ("ms_build", C.c_double),
-                ("reserved", C.c_uint64 * 6)]
+                ("ingest_flags", C.c_uint64), ("reserved", C.c_uint64 * 5)]
 
     def as_dict(self) -> Dict[str, float]:
         return {k: getattr(self, k) for k, _t in self._fields_ if k != "reserved"}
@@ -123,6 +123,7 @@ def lib():
     P, I32, U32, U64, D, SZ = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64, C.c_double, C.c_size_t
     sig = {
         "pr_version": (C.c_char_p, []),
+        "pr_build_id": (C.c_char_p, []),
         "pr_opts_default": (None, [C.POINTER(Opts)]),
         "pr_create": (I32, [C.POINTER(P), C.POINTER(Opts)]),
         "pr_destroy": (None, [P]),
@@ -140,6 +141,7 @@ def lib():
         "pr_get_ranks": (I32, [P, P, U64]),
         "pr_topk": (I32, [P, U32, P, P, P, C.POINTER(U32)]),
         "pr_write_top_page": (I32, [P, C.c_char_p]),
+        "pr_write_rank_dump": (I32, [P, C.c_char_p]),
         "pr_id_string": (I32, [P, U32, C.c_char_p, SZ, C.POINTER(SZ)]),
         "pr_pair": (I32, [P, U64, C.POINTER(U32), C.c_char_p, SZ, C.POINTER(SZ)]),
         "pr_get_degrees": (I32, [P, P, P, P, U64]),
@@ -162,6 +164,17 @@ def lib():
         f.argtypes = args
     _lib = L
     return L
+
+
+def build_id() -> str:
+    """Source hash the loaded library was built from (``pr_build_id``)."""
+    return lib().pr_build_id().decode()
+
+
+def source_hash() -> str:
+    """Hash of the checked-out engine sources (what a fresh build would report)."""
+    import source_hash as _sh
+    return _sh.source_hash()
 
 
 def _ptr(a: Optional[np.ndarray]):
@@ -310,6 +323,10 @@ class Engine:
 
     def write_top_page(self, path: str = "./topPage"):
         self._check(lib().pr_write_top_page(self._h, path.encode()))
+
+    def write_rank_dump(self, path: str):
+        """Every ranked page by id: `id \\t title \\t rank` lines (pr_write_rank_dump)."""
+        self._check(lib().pr_write_rank_dump(self._h, path.encode()))
 
     def id_string(self, v: int) -> bytes:
         ln = C.c_size_t(0)

@@ -25,9 +25,25 @@ def oracle_mod():
     return O
 
 
+def _gpu_host() -> bool:
+    return os.path.exists("/dev/kfd")
+
+
 @pytest.fixture(scope="session")
 def engine_mod():
+    """The engine library, checked against the checked-out sources: the id baked into it
+    (pr_build_id) must equal the hash of csrc/ + include/ + Makefile.  On a CPU-only host a
+    stale or missing library is rebuilt before anything loads it (make is incremental); on a
+    GPU box the library travels prebuilt, so a mismatch fails the session instead of testing
+    some other binary as HEAD."""
     import prmi355x as P
-    if not os.path.exists(P.LIB_PATH):
+    import source_hash as S
+    want = S.source_hash()
+    if S.library_build_id(P.LIB_PATH) != want:
+        if _gpu_host() or P._lib is not None:
+            pytest.fail(f"stale or missing {P.LIB_PATH}: built from "
+                        f"{S.library_build_id(P.LIB_PATH)}, sources are {want}")
         P.build()
+    assert S.library_build_id(P.LIB_PATH) == want
+    assert P.build_id() == want
     return P

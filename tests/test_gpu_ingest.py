@@ -115,3 +115,27 @@ def test_wiki_config1_ranks(P, O):
     same_graph(eng, g, all_ids=False)
     eng.run(10)
     parity.assert_ranks_close(eng.ranks(), g.run(10)["ranks"])
+
+
+def test_oversized_text_falls_back_to_host_parser(engine_mod, oracle_mod, monkeypatch):
+    """a text input too large for the device ingest (2^30 id tokens; lowered here
+    with PR_INGEST_MAX_TOKENS) is parsed on the host instead of failing; the graph and the
+    ranks are the same as through the device path."""
+    P, O = engine_mod, oracle_mod
+    arcs, mapping = G.wiki_text(seed=9, pages=2000, arcs_target=15000)
+    ref = P.Engine()
+    ref.ingest_buffers(arcs, mapping)
+    assert ref.info()["ingest_flags"] == 0
+    monkeypatch.setenv("PR_INGEST_MAX_TOKENS", "1000")
+    eng = P.Engine()
+    eng.ingest_buffers(arcs, mapping)
+    info = eng.info()
+    assert info["ingest_flags"] == 1
+    g = O.Graph.from_text(arcs, mapping)
+    assert (info["n_vertices"], info["nnz"], info["n_tot"]) == (g.n, g.nnz, g.n_tot)
+    assert eng.edge_digest() == ref.edge_digest() == g.edge_digest()
+    ref.run(10)
+    eng.run(10)
+    assert np.array_equal(eng.ranks(), ref.ranks())
+    with pytest.raises(P.ArrayIndexOutOfBoundsException):   # the host path keeps the AIOOBE
+        P.Engine().ingest_buffers(arcs + b"bad line\n", mapping)

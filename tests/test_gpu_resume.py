@@ -145,3 +145,24 @@ def test_resume_keeps_failure_round(P):
     eng.set_ranks(eng.ranks(), 1)
     with pytest.raises(P.UnsupportedOperationException, match="iteration 2"):
         eng.run(5)
+
+
+def test_resume_keeps_failure_round_in_a_rank_group(P):
+    """pr_run_group reports the failing round with the seed's rounds added, and a
+    seeded group does not re-check round 1's dangling mass."""
+    arcs, mapping = b"1\t2\n1\t3\n2\t3\n3\t1\n4\t3\n", b"1\tA\n2\tB\n3\tC\n4\tD\n5\tE\n"
+    eng = P.Engine()
+    eng.ingest_buffers(arcs, mapping)
+    eng.run(1)
+    r1 = eng.ranks()
+    grp = P.LocalGroup(2)
+    grp.each("ingest_buffers", arcs, mapping)
+    with pytest.raises(P.UnsupportedOperationException, match="iteration 2"):
+        grp.run(5)
+    grp.each("set_ranks", r1, 1)
+    with pytest.raises(P.UnsupportedOperationException, match="iteration 2"):
+        grp.run(5)
+    grp.members[1].set_ranks(None)          # members seeded differently: refused
+    with pytest.raises(P.PageRankError, match="seeded differently"):
+        grp.run(1)
+    grp.close()

@@ -186,3 +186,18 @@ def test_oracle_normalized_and_resume(oracle_mod):
     r4 = g.run(4)["ranks"]
     r10 = g.run(6, r_init=r4)["ranks"]
     assert np.array_equal(r10.view(np.uint64), plain.view(np.uint64))
+
+
+def test_parallel_edge_sort_builds_the_same_csr(oracle_mod):
+    """R-MAT scale 18 (4.2M raw arcs) takes the oracle's parallel MSD+LSD sort path (used for
+    the scale 24-28 config tests): the CSR equals a numpy sort + unique of the same arcs."""
+    O = oracle_mod
+    s, d = O.rmat_edges(18, 16, 11)
+    assert len(s) >= 1 << 22
+    g = O.Graph.from_rmat(18, 16, 11)
+    keys = np.unique((d.astype(np.uint64) << np.uint64(32)) | s.astype(np.uint64))
+    rp, col = g.csr()
+    assert g.nnz == len(keys)
+    assert np.array_equal(col, (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+    indeg = np.bincount((keys >> np.uint64(32)).astype(np.int64), minlength=g.n)
+    assert np.array_equal(np.diff(rp.astype(np.int64)), indeg)
