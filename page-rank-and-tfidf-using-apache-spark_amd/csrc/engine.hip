@@ -411,6 +411,9 @@ struct StreamArgs {
   uint32_t dbg;              // PR_DBG timing experiments: 1 no stores, 2 no gathers, 4 no starts
   uint32_t x_bytes;          // bytes of x (< 2^31: the buffer-load range check drops LDS lanes
                              // and PAD_COL padding)
+  uint32_t l2mode;           // PR_L2MODE: 0 = L2 tasks interleaved 1/nlds per LDS phase,
+                             //            1 = all L2 tasks in one final phase
+  uint32_t ntcol;            // PR_NTCOL: non-temporal column loads, bit 0 LDS tasks, bit 1 L2
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
@@ -544,12 +547,22 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // groups are padded to whole tasks: these loads never leave the stream buffers
     if (lds_task) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
-      cn[0] = cp[0];
-      cn[1] = cp[1];
+      if (A.ntcol & 1u) {
+        cn[0] = __builtin_nontemporal_load(cp);
+        cn[1] = __builtin_nontemporal_load(cp + 1);
+      } else {
+        cn[0] = cp[0];
+        cn[1] = cp[1];
+      }
     } else {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
+      if (A.ntcol & 2u) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) cn[q] = cp[q];
+        for (int q = 0; q < 4; ++q) cn[q] = __builtin_nontemporal_load(cp + q);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cn[q] = cp[q];
+      }
     }
     const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
     bnx = bits[so / EPL];
@@ -558,16 +571,20 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
   // with 1/nlds of the L2 part's tasks (LDS-bound and L2-bound work side by side); with no
   // LDS blocks the single phase is the whole stream.
-  const uint32_t nph = A.nlds ? A.nlds : 1u;
+  const bool l2last = A.l2mode == 1u && A.nlds;  // one final phase for every L2 task
+  const uint32_t nph = A.nlds ? A.nlds + (l2last ? 1u : 0u) : 1u;
   for (uint32_t gi = 0; gi < nph; ++gi) {
     uint32_t tb = l2b, te = l2b, rb = l2b, re = l2e;  // LDS-block tasks, L2 share
     uint64_t lbase = 0;
-    if (A.nlds) {
+    if (l2last && gi == A.nlds) {
+      // the L2 phase: no LDS block, the whole L2 group (segments swept in order)
+    } else if (A.nlds) {
       tb = A.gtask[j * ngs + gi];
       te = A.gtask[j * ngs + gi + 1];
       lbase = A.gbase[j * ngs + gi];
       rb = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * gi) / A.nlds);
       re = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * (gi + 1)) / A.nlds);
+      if (l2last) rb = re = l2b;
       const uint32_t hb = A.hot_base[j] + gi * A.H;
       __syncthreads();  // every wave is done with the previous block
       if (te > tb) {
@@ -1462,6 +1479,8 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.nlds = std::max(0, std::min(64, env_int("PR_NLDS", nlds_def)));
   T.stream_wg = std::max(1, std::min(2, env_int("PR_STREAM_WG", T.stream_wg)));
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
+  T.l2mode = env_int("PR_L2MODE", T.l2mode);
+  T.ntcol = env_int("PR_NTCOL", T.ntcol);
   const uint32_t n = in.n;
   const uint64_t m = in.m;
   g->n = n;
@@ -1943,6 +1962,8 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   S.nlds = g->nlds;
   S.H = g->hot_h;
   S.colmask = g->tune.colmask;
+  S.l2mode = static_cast<uint32_t>(g->tune.l2mode);
+  S.ntcol = static_cast<uint32_t>(g->tune.ntcol);
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   RowArgs A{};

@@ -71,8 +71,8 @@ def test_rank_dump_multi_title_and_unmapped(engine_mod, oracle_mod, tmp_path):
     P, O = engine_mod, oracle_mod
     rng = np.random.default_rng(5)
     n, m = 3000, 20000
-    s = rng.integers(0, n, m).astype(np.uint32)
-    d = (rng.zipf(1.6, m) % n).astype(np.uint32)
+    s = rng.integers(0, n // 2, m).astype(np.uint32)          # pages >= n/2 are dangling
+    d = np.where(rng.random(m) < 0.5, rng.zipf(1.6, m) % n, rng.integers(0, n, m)).astype(np.uint32)
     mapw = rng.integers(0, 3, n).astype(np.uint32)
     g = O.Graph.from_edges(s, d, n, mapw, n_tot=int(mapw.sum()))
     r = g.run(8)["ranks"]
