@@ -414,6 +414,8 @@ struct StreamArgs {
   uint32_t l2mode;           // PR_L2MODE: 0 = L2 tasks interleaved 1/nlds per LDS phase,
                              //            1 = all L2 tasks in one final phase
   uint32_t ntcol;            // PR_NTCOL: non-temporal column loads, bit 0 LDS tasks, bit 1 L2
+  uint64_t* stamps;          // PR_STAMPS diagnostics: per (workgroup, phase) the phase start
+                             // and every wave's end (s_memrealtime, 100 MHz); nullptr = off
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
@@ -593,6 +595,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       }
       __syncthreads();
     }
+    uint64_t* stp = A.stamps ? A.stamps + (static_cast<uint64_t>(blockIdx.x) * nph + gi) * 17u : nullptr;
+    if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
     const uint32_t nL = te - tb, nR = re - rb, nm = min(nL, nR);
     // virtual index u -> task: alternate LDS / L2 tasks while both last, then the rest
     auto is_lds = [&](uint32_t u) -> bool {
@@ -711,6 +715,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     }
+    if (stp && lane == 0) stp[1 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -1963,6 +1968,16 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   S.H = g->hot_h;
   S.colmask = g->tune.colmask;
   S.l2mode = static_cast<uint32_t>(g->tune.l2mode);
+  const bool stamps = t == 1 && getenv("PR_STAMPS") && g->nlds && g->ntask;
+  const uint32_t nph = g->nlds + (g->tune.l2mode == 1 ? 1u : 0u);
+  std::vector<uint64_t> hst;
+  uint64_t* dst = nullptr;
+  if (stamps) {
+    hst.assign(static_cast<size_t>(NSLICE) * 32 * nph * 17, 0);
+    HIPTRY(hipMalloc(&dst, 8 * hst.size()));
+    HIPTRY(hipMemsetAsync(dst, 0, 8 * hst.size(), s));
+  }
+  S.stamps = dst;
   S.ntcol = static_cast<uint32_t>(g->tune.ntcol);
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
@@ -1993,6 +2008,42 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   A.SL = g->SL;
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
   if (g->ntask) launch_stream(g, S, s);
+  if (stamps) {  // PR_STAMPS: per-phase time of the stream launch (diagnostics only)
+    HIPTRY(hipMemcpyAsync(hst.data(), dst, 8 * hst.size(), hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(dst);
+    const uint32_t nwg = NSLICE * 32;
+    double prev_end = 0;
+    uint64_t t0 = ~0ull;
+    for (uint32_t b = 0; b < nwg; ++b) t0 = std::min<uint64_t>(t0, hst[(static_cast<size_t>(b) * nph) * 17]);
+    for (uint32_t gi = 0; gi < nph; ++gi) {
+      double st_avg = 0, end_avg = 0, end_max = 0, span_avg = 0;
+      for (uint32_t b = 0; b < nwg; ++b) {
+        const uint64_t* q = &hst[(static_cast<size_t>(b) * nph + gi) * 17];
+        uint64_t e = 0;
+        for (int w = 1; w <= 16; ++w) e = std::max(e, q[w]);
+        st_avg += (q[0] - t0) * 0.01;
+        end_avg += (e - t0) * 0.01;
+        end_max = std::max(end_max, (e - t0) * 0.01);
+        span_avg += (e - q[0]) * 0.01;
+      }
+      st_avg /= nwg; end_avg /= nwg; span_avg /= nwg;
+      uint64_t lt = 0, l2t = 0;  // tasks of the phase over the 8 slices
+      const uint32_t ngs = g->nlds + 1;
+      for (int j = 0; j < NSLICE; ++j) {
+        const uint32_t l2n = g->gtask[j * ngs + g->nlds + 1] - g->gtask[j * ngs + g->nlds];
+        if (gi < g->nlds) {
+          lt += g->gtask[j * ngs + gi + 1] - g->gtask[j * ngs + gi];
+          if (g->tune.l2mode != 1) l2t += (static_cast<uint64_t>(l2n) * (gi + 1)) / g->nlds - (static_cast<uint64_t>(l2n) * gi) / g->nlds;
+        } else {
+          l2t += l2n;
+        }
+      }
+      fprintf(stderr, "[stamps] phase %2u start %8.1f us  end avg %8.1f max %8.1f  span avg %7.1f  fill+wait %6.1f  lds tasks %7llu  l2 tasks %7llu\n",
+              gi, st_avg, end_avg, end_max, span_avg, st_avg - prev_end, (unsigned long long)lt, (unsigned long long)l2t);
+      prev_end = end_avg;
+    }
+  }
   if (g->nb_rows) {
     const dim3 gr(g->nb_rows), bl(BLOCK);
     if (A.NS <= 512) {
