@@ -416,6 +416,8 @@ struct StreamArgs {
   uint32_t ntcol;            // PR_NTCOL: non-temporal column loads, bit 0 LDS tasks, bit 1 L2
   uint64_t* stamps;          // PR_STAMPS diagnostics: per (workgroup, phase) the phase start
                              // and every wave's end (s_memrealtime, 100 MHz); nullptr = off
+  uint32_t l2w;              // PR_L2W: waves per workgroup dedicated to the L2 group (0 = the
+                             // L2 tasks are shared out over the LDS phases, see l2mode)
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
@@ -523,8 +525,34 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   const uint32_t j = blockIdx.x % NSLICE;
   const uint32_t wpb = blockDim.x >> 6;
   const int lane = threadIdx.x & 63;
-  const uint32_t w = (blockIdx.x / NSLICE) * wpb + (threadIdx.x >> 6);
-  const uint32_t nw = (gridDim.x / NSLICE) * wpb;
+  const uint32_t wv = threadIdx.x >> 6;
+  // Roles (PR_L2W): with l2w > 0 the last l2w waves of every workgroup sweep the L2 group
+  // (gathers through the XCD's L2) for the whole launch while the other LW waves run the LDS
+  // phases: latency-bound gathers beside bandwidth-bound LDS tasks.  The LW waves then sync
+  // with an LDS-counter barrier of their own (the L2 waves never wait).
+  const bool split = A.l2w != 0u && A.nlds != 0u;
+  const uint32_t LW = split ? wpb - A.l2w : wpb;
+  const bool l2role = split && wv >= LW;
+  const uint32_t rw = l2role ? A.l2w : LW;  // waves per workgroup in this wave's role
+  const uint32_t w = (blockIdx.x / NSLICE) * rw + (l2role ? wv - LW : wv);
+  const uint32_t nw = (gridDim.x / NSLICE) * rw;
+  __shared__ uint32_t bar_cnt;
+  uint32_t bar_gen = 0;
+  if (threadIdx.x == 0) bar_cnt = 0;
+  __syncthreads();
+  auto block_barrier = [&]() {
+    if (!split) {
+      __syncthreads();
+      return;
+    }
+    // the LW LDS-role waves only: arrive on an LDS counter, spin until all LW arrived
+    ++bar_gen;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_fetch_add(&bar_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&bar_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < bar_gen * LW)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
   const double* __restrict__ x = A.x_in;
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(x), static_cast<short>(0),
@@ -573,27 +601,28 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
   // with 1/nlds of the L2 part's tasks (LDS-bound and L2-bound work side by side); with no
   // LDS blocks the single phase is the whole stream.
-  const bool l2last = A.l2mode == 1u && A.nlds;  // one final phase for every L2 task
-  const uint32_t nph = A.nlds ? A.nlds + (l2last ? 1u : 0u) : 1u;
-  for (uint32_t gi = 0; gi < nph; ++gi) {
+  const bool l2last = A.l2mode == 1u && A.nlds && !split;  // one final phase for every L2 task
+  const uint32_t nph = A.nlds ? A.nlds + ((l2last || split) ? 1u : 0u) : 1u;  // (stamp slots)
+  const uint32_t g0 = l2role ? A.nlds : 0u, g1 = split ? (l2role ? A.nlds + 1u : A.nlds) : nph;
+  for (uint32_t gi = g0; gi < g1; ++gi) {
     uint32_t tb = l2b, te = l2b, rb = l2b, re = l2e;  // LDS-block tasks, L2 share
     uint64_t lbase = 0;
-    if (l2last && gi == A.nlds) {
-      // the L2 phase: no LDS block, the whole L2 group (segments swept in order)
+    if (gi == A.nlds && (l2last || l2role)) {
+      // the L2 phase / role: no LDS block, the whole L2 group (segments swept in order)
     } else if (A.nlds) {
       tb = A.gtask[j * ngs + gi];
       te = A.gtask[j * ngs + gi + 1];
       lbase = A.gbase[j * ngs + gi];
       rb = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * gi) / A.nlds);
       re = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * (gi + 1)) / A.nlds);
-      if (l2last) rb = re = l2b;
+      if (l2last || split) rb = re = l2b;
       const uint32_t hb = A.hot_base[j] + gi * A.H;
-      __syncthreads();  // every wave is done with the previous block
+      block_barrier();  // every wave is done with the previous block
       if (te > tb) {
-        for (uint32_t i = threadIdx.x; i < A.H; i += blockDim.x) hot[i] = x[hb + i];
+        for (uint32_t i = threadIdx.x; i < A.H; i += LW * 64u) hot[i] = x[hb + i];
         if (threadIdx.x == 0) hot[A.H] = 0.0;  // the padding column
       }
-      __syncthreads();
+      block_barrier();
     }
     uint64_t* stp = A.stamps ? A.stamps + (static_cast<uint64_t>(blockIdx.x) * nph + gi) * 17u : nullptr;
     if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
@@ -1486,6 +1515,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   T.l2mode = env_int("PR_L2MODE", T.l2mode);
   T.ntcol = env_int("PR_NTCOL", T.ntcol);
+  T.l2w = std::max(0, std::min(12, env_int("PR_L2W", T.l2w)));
   const uint32_t n = in.n;
   const uint64_t m = in.m;
   g->n = n;
@@ -1969,7 +1999,7 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   S.colmask = g->tune.colmask;
   S.l2mode = static_cast<uint32_t>(g->tune.l2mode);
   const bool stamps = t == 1 && getenv("PR_STAMPS") && g->nlds && g->ntask;
-  const uint32_t nph = g->nlds + (g->tune.l2mode == 1 ? 1u : 0u);
+  const uint32_t nph = g->nlds + ((g->tune.l2mode == 1 || g->tune.l2w) ? 1u : 0u);
   std::vector<uint64_t> hst;
   uint64_t* dst = nullptr;
   if (stamps) {
@@ -1979,6 +2009,7 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   }
   S.stamps = dst;
   S.ntcol = static_cast<uint32_t>(g->tune.ntcol);
+  S.l2w = static_cast<uint32_t>(g->tune.l2w);
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   RowArgs A{};
@@ -2034,7 +2065,7 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
         const uint32_t l2n = g->gtask[j * ngs + g->nlds + 1] - g->gtask[j * ngs + g->nlds];
         if (gi < g->nlds) {
           lt += g->gtask[j * ngs + gi + 1] - g->gtask[j * ngs + gi];
-          if (g->tune.l2mode != 1) l2t += (static_cast<uint64_t>(l2n) * (gi + 1)) / g->nlds - (static_cast<uint64_t>(l2n) * gi) / g->nlds;
+          if (g->tune.l2mode != 1 && !g->tune.l2w) l2t += (static_cast<uint64_t>(l2n) * (gi + 1)) / g->nlds - (static_cast<uint64_t>(l2n) * gi) / g->nlds;
         } else {
           l2t += l2n;
         }

@@ -297,8 +297,11 @@ def tiny_blocks(monkeypatch):
         monkeypatch.setenv(k, v)
 
 
-@pytest.mark.parametrize("scale,ef,seed", [(14, 16, 21), (16, 8, 22)])
-def test_stream_layout_tiny_blocks(P, O, tiny_blocks, scale, ef, seed):
+@pytest.mark.parametrize("scale,ef,seed,l2w", [(14, 16, 21, 0), (16, 8, 22, 0), (14, 16, 23, 4),
+                                             (16, 8, 24, 7)])
+def test_stream_layout_tiny_blocks(P, O, tiny_blocks, monkeypatch, scale, ef, seed, l2w):
+    """l2w > 0: dedicated L2-group waves beside the LDS-phase waves (PR_L2W)."""
+    monkeypatch.setenv("PR_L2W", str(l2w))
     g = O.Graph.from_rmat(scale, ef, seed)
     exp = g.run(10)["ranks"]
     eng = P.Engine()
