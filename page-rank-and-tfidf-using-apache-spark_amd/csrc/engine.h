@@ -68,7 +68,6 @@ struct Tuning {
   int dbg = 0;          // PR_DBG: timing-only experiments in the stream kernel (see StreamArgs)
   int stream_wg = 1;    // PR_STREAM_WG: stream workgroups per CU (1 with the LDS copy)
   int l2mode = 0;       // PR_L2MODE: 0 = L2 tasks interleaved with the LDS phases, 1 = last
-  int ntcol = 0;        // PR_NTCOL: non-temporal column loads (bit 0 LDS tasks, bit 1 L2 tasks)
   int l2w = 0;          // PR_L2W: waves per stream workgroup dedicated to the L2 group
 };
 

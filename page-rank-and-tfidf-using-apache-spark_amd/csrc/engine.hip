@@ -413,7 +413,6 @@ struct StreamArgs {
                              // and PAD_COL padding)
   uint32_t l2mode;           // PR_L2MODE: 0 = L2 tasks interleaved 1/nlds per LDS phase,
                              //            1 = all L2 tasks in one final phase
-  uint32_t ntcol;            // PR_NTCOL: non-temporal column loads, bit 0 LDS tasks, bit 1 L2
   uint64_t* stamps;          // PR_STAMPS diagnostics: per (workgroup, phase) the phase start
                              // and every wave's end (s_memrealtime, 100 MHz); nullptr = off
   uint32_t l2w;              // PR_L2W: waves per workgroup dedicated to the L2 group (0 = the
@@ -519,7 +518,10 @@ __device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[
       : "memory");
 }
 
-template <int NT>
+// NT: 2 = non-temporal piece stores.  SPLIT: dedicated L2 waves (A.l2w).  STAMPS: PR_STAMPS
+// diagnostics.  The variants are separate instantiations so that the default one carries no
+// register cost for the others.
+template <int NT, bool SPLIT, bool STAMPS>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
   const uint32_t j = blockIdx.x % NSLICE;
@@ -530,16 +532,20 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // (gathers through the XCD's L2) for the whole launch while the other LW waves run the LDS
   // phases: latency-bound gathers beside bandwidth-bound LDS tasks.  The LW waves then sync
   // with an LDS-counter barrier of their own (the L2 waves never wait).
-  const bool split = A.l2w != 0u && A.nlds != 0u;
+  const bool split = SPLIT && A.l2w != 0u && A.nlds != 0u;
   const uint32_t LW = split ? wpb - A.l2w : wpb;
   const bool l2role = split && wv >= LW;
   const uint32_t rw = l2role ? A.l2w : LW;  // waves per workgroup in this wave's role
   const uint32_t w = (blockIdx.x / NSLICE) * rw + (l2role ? wv - LW : wv);
   const uint32_t nw = (gridDim.x / NSLICE) * rw;
-  __shared__ uint32_t bar_cnt;
+  // the barrier counter lives in the spare words after the LDS block's zero slot (the dynamic
+  // LDS request is already the whole 160 KiB: no static __shared__ may be added)
+  uint32_t& bar_cnt = *reinterpret_cast<uint32_t*>(hot + A.H + 1);
   uint32_t bar_gen = 0;
-  if (threadIdx.x == 0) bar_cnt = 0;
-  __syncthreads();
+  if (split) {
+    if (threadIdx.x == 0) bar_cnt = 0;
+    __syncthreads();
+  }
   auto block_barrier = [&]() {
     if (!split) {
       __syncthreads();
@@ -577,22 +583,12 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // groups are padded to whole tasks: these loads never leave the stream buffers
     if (lds_task) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
-      if (A.ntcol & 1u) {
-        cn[0] = __builtin_nontemporal_load(cp);
-        cn[1] = __builtin_nontemporal_load(cp + 1);
-      } else {
-        cn[0] = cp[0];
-        cn[1] = cp[1];
-      }
+      cn[0] = cp[0];
+      cn[1] = cp[1];
     } else {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
-      if (A.ntcol & 2u) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cn[q] = __builtin_nontemporal_load(cp + q);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cn[q] = cp[q];
-      }
+      for (int q = 0; q < 4; ++q) cn[q] = cp[q];
     }
     const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
     bnx = bits[so / EPL];
@@ -624,7 +620,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       }
       block_barrier();
     }
-    uint64_t* stp = A.stamps ? A.stamps + (static_cast<uint64_t>(blockIdx.x) * nph + gi) * 17u : nullptr;
+    uint64_t* stp = STAMPS ? A.stamps + (static_cast<uint64_t>(blockIdx.x) * nph + gi) * 17u : nullptr;
     if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
     const uint32_t nL = te - tb, nR = re - rb, nm = min(nL, nR);
     // virtual index u -> task: alternate LDS / L2 tasks while both last, then the rest
@@ -1514,7 +1510,6 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.stream_wg = std::max(1, std::min(2, env_int("PR_STREAM_WG", T.stream_wg)));
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   T.l2mode = env_int("PR_L2MODE", T.l2mode);
-  T.ntcol = env_int("PR_NTCOL", T.ntcol);
   T.l2w = std::max(0, std::min(12, env_int("PR_L2W", T.l2w)));
   const uint32_t n = in.n;
   const uint64_t m = in.m;
@@ -1968,13 +1963,20 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   const dim3 gr(NSLICE * 32 * per_cu), bl(STREAM_BLOCK);
   static bool attr_set = false;  // allow the >64 KB dynamic LDS request
   if (!attr_set) {
-    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<0>),
-                          reinterpret_cast<const void*>(&spmv_stream<2>)})
+    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<0, false, false>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, false, false>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, false>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, false, true>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, true>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  if (g->tune.nt == 2) hipLaunchKernelGGL((spmv_stream<2>), gr, bl, lds, s, A);
-  else hipLaunchKernelGGL((spmv_stream<0>), gr, bl, lds, s, A);
+  const bool split = A.l2w && A.nlds, st = A.stamps != nullptr;
+  if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
+  else if (split && st) hipLaunchKernelGGL((spmv_stream<2, true, true>), gr, bl, lds, s, A);
+  else if (split) hipLaunchKernelGGL((spmv_stream<2, true, false>), gr, bl, lds, s, A);
+  else if (st) hipLaunchKernelGGL((spmv_stream<2, false, true>), gr, bl, lds, s, A);
+  else hipLaunchKernelGGL((spmv_stream<2, false, false>), gr, bl, lds, s, A);
 }
 
 }  // namespace
@@ -2008,7 +2010,6 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
     HIPTRY(hipMemsetAsync(dst, 0, 8 * hst.size(), s));
   }
   S.stamps = dst;
-  S.ntcol = static_cast<uint32_t>(g->tune.ntcol);
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));

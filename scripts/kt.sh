@@ -3,7 +3,7 @@
 # usage: scripts/kt.sh TAG [VAR=value ...]
 tag=$1; shift
 export TMPDIR=/tmp
-env "$@" timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_$tag -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/kt_$tag.log 2>&1 || exit $?
+env "$@" timeout -k 10 150 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_$tag -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/kt_$tag.log 2>&1 || exit $?
 python3 - "$tag" <<'PY'
 import csv, sys
 tag = sys.argv[1]
