@@ -131,6 +131,27 @@ int pr_comm_init(pr_ctx* ctx, const uint8_t id[128]);
 int pr_comm_init_local(pr_ctx** ctxs, int32_t n);
 int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_stats* stats);
 
+/* Caller-staged exchange: the per-round exchange of the reduceByKey shuffle (:139) and of
+ * the dangling reduce (:125) over a transport the caller owns (MPI, a host collective, ...)
+ * instead of RCCL.  One process per rank, contexts with n_ranks > 1 and
+ * pr_comm_init_external() before the graph is built.  Then per run:
+ *   pr_ext_begin(ctx, T, tol, &unit)            unit = bytes each rank contributes per round
+ *   for t = 1..T:
+ *     pr_ext_round(ctx, t, send)                round t's SpMV; send <- this rank's unit
+ *     <caller all-gathers the p units, rank order, into recv (p * unit bytes)>
+ *     pr_ext_complete(ctx, t, recv, &stop)      peers' units in, next round's addthis;
+ *                                               stop = 1 once the residual is <= tol
+ *   pr_ext_end(ctx, &stats)
+ * pr_ext_complete returns PR_E_EMPTY_DANGLING where the reference dies (:125).  Buffers are
+ * caller-owned host memory.  Outputs of an externally exchanged context are this rank's only:
+ * pr_get_ranks returns its pages' ranks (0.0 elsewhere; the caller sums over ranks) and
+ * pr_topk its pages' top rows. */
+int pr_comm_init_external(pr_ctx* ctx);
+int pr_ext_begin(pr_ctx* ctx, int32_t iterations, double tol, uint64_t* bytes_per_rank);
+int pr_ext_round(pr_ctx* ctx, int32_t t, void* send);
+int pr_ext_complete(pr_ctx* ctx, int32_t t, const void* recv_all, int32_t* stop);
+int pr_ext_end(pr_ctx* ctx, pr_stats* stats);
+
 /* textFile(arcs)/textFile(mapping) + mapToPair(split) + distinct + groupByKey + cache +
  * subtractByKey + distinct().count() (PageRank.java:26-60), then the device CSR build. */
 int pr_ingest_files(pr_ctx* ctx, const char* arcs_path, const char* mapping_path);

@@ -46,6 +46,13 @@ struct pr_ctx {
   int seed_rounds = 0;           // pr_set_ranks: rounds behind the seed (0 = no seed)
   prmi::TfidfState tf;           // the TF-IDF job (Spark.java)
   bool ingest_fallback = false;  // last text ingest went to the host parser (too large)
+  // caller-staged exchange (pr_comm_init_external / pr_ext_*): the caller moves each
+  // round's x slot + exact record between ranks with a transport of its own
+  bool external = false;
+  int ext_iters = 0, ext_done = 0;
+  double ext_tol = 0.0;
+  bool ext_tracked = false;
+  prmi::IterState ext_hs{};
 };
 
 namespace {
@@ -83,8 +90,8 @@ int need_graph(pr_ctx* c) {
 }
 
 int need_comm(pr_ctx* c) {
-  if (c->opts.n_ranks > 1 && !c->comm && c->group.empty())
-    return fail(c, PR_E_ARG, "n_ranks > 1 requires pr_comm_init before building a graph");
+  if (c->opts.n_ranks > 1 && !c->comm && c->group.empty() && !c->external)
+    return fail(c, PR_E_ARG, "n_ranks > 1 requires pr_comm_init (or pr_comm_init_external) before building a graph");
   return PR_OK;
 }
 
@@ -142,7 +149,8 @@ int gather_ranks(pr_ctx* c) {
   }
   rc = prmi::dev_scatter_ranks(&c->dg, c->last_iters, c->stream);
   if (rc) return fail(c, rc, "scatter ranks");
-  if (c->opts.n_ranks > 1 && c->dg.n)
+  // (external exchange: this rank's pages only; the caller sums over its ranks)
+  if (c->opts.n_ranks > 1 && c->dg.n && !c->external)
     NCCLCHK(c, ncclAllReduce(c->dg.r_full, c->dg.r_full, c->dg.n, ncclFloat64, ncclSum, c->comm, c->stream));
   c->h_ranks.resize(c->dg.n);
   if (c->dg.n)
@@ -232,7 +240,7 @@ int topk_candidates(pr_ctx* c, uint64_t k, std::vector<uint32_t>* ids, std::vect
   if (!rc) rc = prmi::dev_topk_candidates(&c->dg, k, ids, rs, c->stream, &err);
   if (rc) return fail(c, rc, "top-K selection: " + err);
   const int p = c->opts.n_ranks;
-  if (p <= 1) return PR_OK;
+  if (p <= 1 || c->external) return PR_OK;  // external exchange: this rank's candidates
   // all-gather the per-rank candidate counts, then the candidates padded to the largest count
   uint64_t* d_cnt = nullptr;
   HIPCHK(c, hipMalloc(&d_cnt, 8ull * p));
@@ -555,6 +563,103 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
   return PR_OK;
 }
 
+int pr_comm_init_external(pr_ctx* c) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  if (c->comm || !c->group.empty()) return fail(c, PR_E_ARG, "context already has a transport");
+  if (c->opts.n_ranks < 2) return fail(c, PR_E_ARG, "external exchange needs n_ranks > 1");
+  c->external = true;
+  return PR_OK;
+}
+
+int pr_ext_begin(pr_ctx* c, int32_t iterations, double tol, uint64_t* bytes_per_rank) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  if (!c->external) return fail(c, PR_E_ARG, "pr_ext_* needs pr_comm_init_external");
+  if (iterations < 1) return fail(c, PR_E_ARG, "iterations < 1");
+  DevGraph* g = &c->dg;
+  if (!g->seeded && g->W0 == 0) return fail(c, PR_E_EMPTY_DANGLING, "java.lang.UnsupportedOperationException: empty collection (iteration 1)");
+  c->ext_iters = iterations;
+  c->ext_done = 0;
+  c->ext_tol = tol;
+  c->ext_tracked = tol > 0.0 || (c->opts.flags & PR_F_TRACK_RESIDUAL);
+  c->ext_hs = prmi::IterState{};
+  c->host_ranks_valid = false;
+  c->last_iters = -1;
+  rc = prmi::dev_reset_state(g, c->stream);
+  if (rc) return fail(c, rc, "reset state");
+  if (bytes_per_rank) *bytes_per_rank = 8ull * g->maxA + 8ull * prmi::REC_WORDS;
+  return PR_OK;
+}
+
+int pr_ext_round(pr_ctx* c, int32_t t, void* send) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  if (!c->external || t != c->ext_done + 1 || t > c->ext_iters || !send)
+    return fail(c, PR_E_ARG, "pr_ext_round: call pr_ext_begin, then rounds 1, 2, ... in order");
+  DevGraph* g = &c->dg;
+  const int mode = c->ext_tracked ? 2 : (t == c->ext_iters ? 1 : 0);
+  rc = prmi::dev_round_compute(g, t, mode, c->stream, nullptr, nullptr);
+  if (rc) return fail(c, rc, "round compute");
+  // this rank's slot of x' and its exact record, in that order
+  char* out = static_cast<char*>(send);
+  const double* xs = prmi::dev_x_out(g, t) + static_cast<uint64_t>(g->rank) * g->maxA;
+  if (g->maxA) HIPCHK(c, hipMemcpyAsync(out, xs, 8ull * g->maxA, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(out + 8ull * g->maxA, g->rec_local, 8ull * prmi::REC_WORDS, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PR_OK;
+}
+
+int pr_ext_complete(pr_ctx* c, int32_t t, const void* recv_all, int32_t* stop) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  if (!c->external || t != c->ext_done + 1 || !recv_all)
+    return fail(c, PR_E_ARG, "pr_ext_complete: after pr_ext_round of the same round");
+  DevGraph* g = &c->dg;
+  const int p = c->opts.n_ranks;
+  const uint64_t unit = 8ull * g->maxA + 8ull * prmi::REC_WORDS;
+  const char* in = static_cast<const char*>(recv_all);
+  double* xf = prmi::dev_x_out(g, t);
+  for (int r = 0; r < p; ++r) {
+    if (r != g->rank && g->maxA)
+      HIPCHK(c, hipMemcpyAsync(xf + static_cast<uint64_t>(r) * g->maxA, in + r * unit, 8ull * g->maxA, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(g->rec_all + static_cast<uint64_t>(r) * prmi::REC_WORDS, in + r * unit + 8ull * g->maxA, 8ull * prmi::REC_WORDS, hipMemcpyHostToDevice, c->stream));
+  }
+  rc = prmi::dev_round_finalize(g, t, c->ext_tracked, c->stream);
+  if (rc) return fail(c, rc, "round finalize");
+  HIPCHK(c, hipMemcpyAsync(&c->ext_hs, g->state, sizeof(c->ext_hs), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->ext_done = t;
+  const bool conv = c->ext_tol > 0.0 && c->ext_hs.resid <= c->ext_tol;
+  if (stop) *stop = conv ? 1 : 0;
+  // the reduce of a round (PageRank.java:125) saw an empty danglingMap: the job dies there
+  if (c->ext_hs.err_iter != 0 && c->ext_hs.err_iter <= t) {
+    const int t0 = g->seeded ? c->seed_rounds : 0;
+    if (stop) *stop = 1;
+    return fail(c, PR_E_EMPTY_DANGLING,
+                "java.lang.UnsupportedOperationException: empty collection (iteration " +
+                    std::to_string(t0 + c->ext_hs.err_iter) + ")");
+  }
+  return PR_OK;
+}
+
+int pr_ext_end(pr_ctx* c, pr_stats* st) {
+  if (!c) return PR_E_ARG;
+  if (!c->external || c->ext_done < 1) return fail(c, PR_E_ARG, "pr_ext_end: no completed round");
+  pr_stats s{};
+  s.nnz = c->dg.nnz;
+  s.n_vertices = c->dg.n;
+  s.iterations = c->ext_done;
+  s.residual = c->ext_tracked ? c->ext_hs.resid : 0.0;
+  s.rank_sum = c->ext_tracked ? c->ext_hs.rank_sum : 0.0;
+  c->last_iters = c->ext_done;
+  c->host_ranks_valid = false;
+  if (st) *st = s;
+  return PR_OK;
+}
+
 int pr_ingest_buffers(pr_ctx* c, const char* arcs, size_t alen, const char* map, size_t mlen) {
   if (!c || (!arcs && alen) || (!map && mlen)) return fail(c, PR_E_ARG, "bad buffers");
   int rc = need_comm(c);
@@ -710,6 +815,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   if (rc) return rc;
   if (iterations < 0) return fail(c, PR_E_ARG, "iterations < 0");
   if (!c->group.empty()) return pr_run_group(c->group.data(), static_cast<int32_t>(c->group.size()), iterations, tol, st);
+  if (c->external) return fail(c, PR_E_ARG, "externally exchanged context: drive the rounds with pr_ext_*");
   DevGraph* g = &c->dg;
   pr_stats s{};
   s.nnz = g->nnz;

@@ -132,6 +132,11 @@ def lib():
         "pr_comm_init": (I32, [P, C.c_char_p]),
         "pr_comm_init_local": (I32, [C.POINTER(P), I32]),
         "pr_run_group": (I32, [C.POINTER(P), I32, I32, D, C.POINTER(Stats)]),
+        "pr_comm_init_external": (I32, [P]),
+        "pr_ext_begin": (I32, [P, I32, D, C.POINTER(U64)]),
+        "pr_ext_round": (I32, [P, I32, P]),
+        "pr_ext_complete": (I32, [P, I32, P, C.POINTER(I32)]),
+        "pr_ext_end": (I32, [P, C.POINTER(Stats)]),
         "pr_ingest_files": (I32, [P, C.c_char_p, C.c_char_p]),
         "pr_ingest_buffers": (I32, [P, C.c_char_p, SZ, C.c_char_p, SZ]),
         "pr_load_edges": (I32, [P, P, P, U64, U32, P, U64]),
@@ -233,6 +238,28 @@ class Engine:
     # ---- comm ----
     def comm_init(self, uid: bytes):
         self._check(lib().pr_comm_init(self._h, uid))
+
+    def comm_init_external(self):
+        """Exchange rounds through the caller (pr_ext_*), e.g. a torch.distributed group."""
+        self._check(lib().pr_comm_init_external(self._h))
+
+    def run_external(self, iterations: int, allgather, tol: float = 0.0) -> Dict[str, float]:
+        """The round loop with a caller-supplied all-gather: ``allgather(send) -> recv`` takes
+        this rank's uint8 unit and returns the p units in rank order (one uint8 array)."""
+        unit = C.c_uint64(0)
+        self._check(lib().pr_ext_begin(self._h, iterations, tol, C.byref(unit)))
+        send = np.zeros(unit.value, np.uint8)
+        stop = C.c_int32(0)
+        for t in range(1, iterations + 1):
+            self._check(lib().pr_ext_round(self._h, t, _ptr(send)))
+            recv = np.ascontiguousarray(allgather(send), np.uint8)
+            assert recv.size == unit.value * self.n_ranks
+            self._check(lib().pr_ext_complete(self._h, t, _ptr(recv), C.byref(stop)))
+            if stop.value:
+                break
+        st = Stats()
+        self._check(lib().pr_ext_end(self._h, C.byref(st)))
+        return st.as_dict()
 
     # ---- input ----
     def ingest_files(self, arcs_path: str, mapping_path: str):
