@@ -630,7 +630,14 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       const uint32_t hb = A.hot_base[j] + gi * A.H;
       block_barrier();  // every wave is done with the previous block
       if (te > tb) {
-        for (uint32_t i = threadIdx.x; i < A.H; i += LW * 64u) hot[i] = x[hb + i];
+        // LDS-DMA fill: one global_load_lds_dwordx4 moves 1 KiB (128 entries) per wave
+        // instruction straight into LDS (no registers); H is even and hb 16-byte aligned
+        const uint32_t nfill = (A.H + 127u) / 128u;
+        for (uint32_t q = wv; q < nfill; q += LW) {
+          const uint32_t e0 = q * 128u + 2u * static_cast<uint32_t>(lane);
+          if (e0 < A.H) __builtin_amdgcn_global_load_lds(x + hb + e0, hot + q * 128u, 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (threadIdx.x == 0) hot[A.H] = 0.0;  // the padding column
       }
       block_barrier();
@@ -1731,7 +1738,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     G.H = HOT_MAX;
     G.nlds = 0;
     if (g->sm && g->X < (1ull << 28) && T.hot_lds > 0) {
-      G.H = std::min<uint32_t>(HOT_MAX, T.hot_lds);
+      G.H = std::min<uint32_t>(HOT_MAX, T.hot_lds) & ~1u;  // even: 16-byte LDS-DMA fills
       G.nlds = std::min<uint32_t>(static_cast<uint32_t>(T.nlds), g->SL / G.H);
     }
     g->nlds = G.nlds;
