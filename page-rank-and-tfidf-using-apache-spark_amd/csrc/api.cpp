@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -45,6 +46,11 @@ struct pr_ctx {
   std::vector<pr_ctx*> group;    // single-process rank group (pr_comm_init_local)
   int seed_rounds = 0;           // pr_set_ranks: rounds behind the seed (0 = no seed)
   prmi::TfidfState tf;           // the TF-IDF job (Spark.java)
+  // multi-rank exchange: a comm stream beside the compute stream, chunk events
+  hipStream_t comm_stream = nullptr;
+  std::vector<hipEvent_t> ev_chunk;
+  hipEvent_t ev_rec = nullptr, ev_done = nullptr;
+  int xchunks = 4;                // PR_XCHUNKS: row-launch chunks of the x' exchange
   bool ingest_fallback = false;  // last text ingest went to the host parser (too large)
   // caller-staged exchange (pr_comm_init_external / pr_ext_*): the caller moves each
   // round's x slot + exact record between ranks with a transport of its own
@@ -92,6 +98,15 @@ int need_graph(pr_ctx* c) {
 int need_comm(pr_ctx* c) {
   if (c->opts.n_ranks > 1 && !c->comm && c->group.empty() && !c->external)
     return fail(c, PR_E_ARG, "n_ranks > 1 requires pr_comm_init (or pr_comm_init_external) before building a graph");
+  return PR_OK;
+}
+
+// comm stream + events of the chunked exchange (created on first use)
+int ensure_xchg(pr_ctx* c) {
+  if (!c->comm_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+  if (!c->ev_rec) HIPCHK(c, hipEventCreateWithFlags(&c->ev_rec, hipEventDisableTiming));
+  if (!c->ev_done) HIPCHK(c, hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+  if (const char* e = getenv("PR_XCHUNKS")) c->xchunks = std::max(1, atoi(e));
   return PR_OK;
 }
 
@@ -417,6 +432,13 @@ void pr_destroy(pr_ctx* c) {
     prmi::tf_free(&c->tf);
     prmi::dev_free(&c->dg);
     for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_chunk) (void)hipEventDestroy(e);
+    if (c->ev_rec) (void)hipEventDestroy(c->ev_rec);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    if (c->comm_stream) {
+      (void)hipStreamSynchronize(c->comm_stream);
+      (void)hipStreamDestroy(c->comm_stream);
+    }
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -505,36 +527,72 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
   }
   int done = iterations;
   prmi::IterState hs{};
+  std::vector<std::vector<prmi::XChunk>> plans(n);
+  for (int i = 0; i < n; ++i) {
+    pr_ctx* m = ctxs[i];
+    HIPCHK(c0, hipSetDevice(m->device));
+    int rc = ensure_xchg(m);
+    if (rc) return fail(c0, rc, "exchange streams");
+    plans[i] = prmi::dev_exchange_plan(&m->dg, m->xchunks);
+    while (m->ev_chunk.size() < plans[i].size()) {
+      hipEvent_t e;
+      HIPCHK(c0, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      m->ev_chunk.push_back(e);
+    }
+  }
+  for (int i = 1; i < n; ++i)
+    if (plans[i].size() != plans[0].size()) return fail(c0, PR_E_ARG, "local group: exchange plans differ");
   for (int t = 1; t <= iterations; ++t) {
     const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
+    // the schedule of pr_run's chunked exchange, with device copies for ncclSend/Recv: each
+    // member's rows run in chunks; member q's comm stream copies chunk k of every peer's
+    // slot as soon as that peer's chunk event fires, then the records, then finalize
     for (int i = 0; i < n; ++i) {
-      HIPCHK(c0, hipSetDevice(ctxs[i]->device));
-      int rc = prmi::dev_round_compute(&ctxs[i]->dg, t, mode, ctxs[i]->stream, nullptr, nullptr);
+      pr_ctx* m = ctxs[i];
+      HIPCHK(c0, hipSetDevice(m->device));
+      int rc = prmi::dev_round_stream(&m->dg, t, m->stream, nullptr);
+      for (size_t k = 0; !rc && k < plans[i].size(); ++k) {
+        rc = prmi::dev_round_rows(&m->dg, t, mode, plans[i][k].b0, plans[i][k].b1, m->stream);
+        if (!rc && hipEventRecord(m->ev_chunk[k], m->stream) != hipSuccess) rc = PR_E_HIP;
+      }
+      if (!rc) rc = prmi::dev_round_rows(&m->dg, t, mode, m->dg.nb_rows_a, m->dg.nb_rows, m->stream);
+      if (!rc) rc = prmi::dev_round_reduce(&m->dg, m->stream, nullptr);
       if (rc) return fail(c0, rc, "round compute");
+      HIPCHK(c0, hipEventRecord(m->ev_rec, m->stream));
     }
-    for (int i = 0; i < n; ++i) HIPCHK(c0, hipStreamSynchronize(ctxs[i]->stream));
-    // the all-gathers, as copies on each receiver's stream: slot r of x', record r
     for (int q = 0; q < n; ++q) {
-      DevGraph* dst = &ctxs[q]->dg;
-      HIPCHK(c0, hipSetDevice(ctxs[q]->device));
+      pr_ctx* mq = ctxs[q];
+      DevGraph* dst = &mq->dg;
+      HIPCHK(c0, hipSetDevice(mq->device));
+      for (size_t k = 0; k < plans[q].size(); ++k)
+        for (int r = 0; r < n; ++r) {
+          if (r == q) continue;
+          DevGraph* src = &ctxs[r]->dg;
+          HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ctxs[r]->ev_chunk[k], 0));
+          const uint64_t base = static_cast<uint64_t>(r) * src->maxA;
+          for (const prmi::XPiece& pc : plans[q][k].pieces)
+            HIPCHK(c0, hipMemcpyPeerAsync(prmi::dev_x_out(dst, t) + base + pc.off, mq->device,
+                                          prmi::dev_x_out(src, t) + base + pc.off, ctxs[r]->device,
+                                          8ull * pc.cnt, mq->comm_stream));
+        }
       for (int r = 0; r < n; ++r) {
         DevGraph* src = &ctxs[r]->dg;
-        const uint64_t off = static_cast<uint64_t>(r) * src->maxA;
-        if (q != r && src->maxA)
-          HIPCHK(c0, hipMemcpyPeerAsync(prmi::dev_x_out(dst, t) + off, ctxs[q]->device,
-                                        prmi::dev_x_out(src, t) + off, ctxs[r]->device,
-                                        8ull * src->maxA, ctxs[q]->stream));
+        HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ctxs[r]->ev_rec, 0));
         HIPCHK(c0, hipMemcpyPeerAsync(dst->rec_all + static_cast<uint64_t>(r) * prmi::REC_WORDS,
-                                      ctxs[q]->device, src->rec_local, ctxs[r]->device,
-                                      8ull * prmi::REC_WORDS, ctxs[q]->stream));
+                                      mq->device, src->rec_local, ctxs[r]->device,
+                                      8ull * prmi::REC_WORDS, mq->comm_stream));
       }
+      int rc = prmi::dev_round_finalize(dst, t, tracked, mq->comm_stream);
+      if (rc) return fail(c0, rc, "round finalize");
+      HIPCHK(c0, hipEventRecord(mq->ev_done, mq->comm_stream));
     }
+    // round t+1 starts once every member has its x' and a (and every copy out of this
+    // member's slot has run, so the slot may be rewritten two rounds later)
     for (int i = 0; i < n; ++i) {
       HIPCHK(c0, hipSetDevice(ctxs[i]->device));
-      int rc = prmi::dev_round_finalize(&ctxs[i]->dg, t, tracked, ctxs[i]->stream);
-      if (rc) return fail(c0, rc, "round finalize");
+      for (int q = 0; q < n; ++q) HIPCHK(c0, hipStreamWaitEvent(ctxs[i]->stream, ctxs[q]->ev_done, 0));
     }
-    for (int i = 0; i < n; ++i) HIPCHK(c0, hipStreamSynchronize(ctxs[i]->stream));
+    if (tol == 0.0) continue;
     HIPCHK(c0, hipMemcpyAsync(&hs, c0->dg.state, sizeof(hs), hipMemcpyDeviceToHost, c0->stream));
     HIPCHK(c0, hipStreamSynchronize(c0->stream));
     if (tol > 0.0 && hs.resid <= tol) {
@@ -542,9 +600,15 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       break;
     }
   }
-  for (int i = 0; i < n; ++i) HIPCHK(c0, hipStreamSynchronize(ctxs[i]->stream));
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(c0, hipSetDevice(ctxs[i]->device));
+    HIPCHK(c0, hipStreamSynchronize(ctxs[i]->stream));
+    HIPCHK(c0, hipStreamSynchronize(ctxs[i]->comm_stream));
+  }
   HIPCHK(c0, hipSetDevice(c0->device));
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  HIPCHK(c0, hipMemcpyAsync(&hs, c0->dg.state, sizeof(hs), hipMemcpyDeviceToHost, c0->stream));
+  HIPCHK(c0, hipStreamSynchronize(c0->stream));
   s.iterations = done;
   s.ms_total = ms;
   s.ms_per_iter = ms / done;
@@ -846,21 +910,64 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
   int done = iterations;
   prmi::IterState hs{};
+  const int p = c->opts.n_ranks;
+  std::vector<prmi::XChunk> plan;
+  if (p > 1) {
+    rc = ensure_xchg(c);
+    if (rc) return rc;
+    plan = prmi::dev_exchange_plan(g, c->xchunks);
+    while (c->ev_chunk.size() < plan.size()) {
+      hipEvent_t e;
+      HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->ev_chunk.push_back(e);
+    }
+  }
   for (int t = 1; t <= iterations; ++t) {
     const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
     hipEvent_t e0 = t <= nk ? c->kev[2 * (t - 1)] : nullptr;
     hipEvent_t e1 = t <= nk ? c->kev[2 * (t - 1) + 1] : nullptr;
-    rc = prmi::dev_round_compute(g, t, mode, c->stream, e0, e1);
-    if (rc) return fail(c, rc, "round compute");
-    if (c->opts.n_ranks > 1) {
+    if (p == 1) {
+      rc = prmi::dev_round_compute(g, t, mode, c->stream, e0, e1);
+      if (rc) return fail(c, rc, "round compute");
+      rc = prmi::dev_round_finalize(g, t, tracked, c->stream);
+      if (rc) return fail(c, rc, "round finalize");
+    } else {
+      // Chunked exchange replacing the reduceByKey shuffle (PageRank.java:139): the row
+      // launch runs in chunks of class-A row blocks; as chunk k's x' slot pieces are final,
+      // the comm stream sends them to every peer (grouped ncclSend/ncclRecv over xGMI, one
+      // direct link per peer) while the compute stream runs the next chunk.  The exact
+      // records are all-gathered after the last rows, finalize runs on the comm stream, and
+      // the next round's stream launch waits for it.
       double* xf = prmi::dev_x_out(g, t);
-      NCCLCHK(c, ncclGroupStart());
-      NCCLCHK(c, ncclAllGather(xf + static_cast<uint64_t>(g->rank) * g->maxA, xf, g->maxA, ncclFloat64, c->comm, c->stream));
-      NCCLCHK(c, ncclAllGather(g->rec_local, g->rec_all, prmi::REC_WORDS, ncclUint64, c->comm, c->stream));
-      NCCLCHK(c, ncclGroupEnd());
+      rc = prmi::dev_round_stream(g, t, c->stream, e0);
+      if (rc) return fail(c, rc, "round compute");
+      for (size_t k = 0; k < plan.size(); ++k) {
+        rc = prmi::dev_round_rows(g, t, mode, plan[k].b0, plan[k].b1, c->stream);
+        if (rc) return fail(c, rc, "round rows");
+        HIPCHK(c, hipEventRecord(c->ev_chunk[k], c->stream));
+      }
+      rc = prmi::dev_round_rows(g, t, mode, g->nb_rows_a, g->nb_rows, c->stream);  // class B
+      if (!rc) rc = prmi::dev_round_reduce(g, c->stream, e1);
+      if (rc) return fail(c, rc, "round rows");
+      HIPCHK(c, hipEventRecord(c->ev_rec, c->stream));
+      for (size_t k = 0; k < plan.size(); ++k) {
+        HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_chunk[k], 0));
+        NCCLCHK(c, ncclGroupStart());
+        for (const prmi::XPiece& pc : plan[k].pieces)
+          for (int q = 0; q < p; ++q) {
+            if (q == g->rank) continue;
+            NCCLCHK(c, ncclSend(xf + static_cast<uint64_t>(g->rank) * g->maxA + pc.off, pc.cnt, ncclFloat64, q, c->comm, c->comm_stream));
+            NCCLCHK(c, ncclRecv(xf + static_cast<uint64_t>(q) * g->maxA + pc.off, pc.cnt, ncclFloat64, q, c->comm, c->comm_stream));
+          }
+        NCCLCHK(c, ncclGroupEnd());
+      }
+      HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_rec, 0));
+      NCCLCHK(c, ncclAllGather(g->rec_local, g->rec_all, prmi::REC_WORDS, ncclUint64, c->comm, c->comm_stream));
+      rc = prmi::dev_round_finalize(g, t, tracked, c->comm_stream);
+      if (rc) return fail(c, rc, "round finalize");
+      HIPCHK(c, hipEventRecord(c->ev_done, c->comm_stream));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));  // round t+1 needs x' and a
     }
-    rc = prmi::dev_round_finalize(g, t, tracked, c->stream);
-    if (rc) return fail(c, rc, "round finalize");
     if (tol > 0.0) {
       HIPCHK(c, hipMemcpyAsync(&hs, g->state, sizeof(hs), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));

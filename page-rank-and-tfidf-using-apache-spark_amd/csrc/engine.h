@@ -162,6 +162,21 @@ void dev_free(DevGraph* g);
 // mode: 0 = x' only, 1 = also write r', 2 = tracked (r', exact residual + rank sum).
 int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev0,
                       hipEvent_t ev1);
+// The same in three steps (the row launch may be cut into block ranges [b0, b1), e.g. for the
+// chunked exchange): the stream launch; rows of blocks [b0, b1); the record reduction.
+int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0);
+int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipStream_t s);
+int dev_round_reduce(DevGraph* g, hipStream_t s, hipEvent_t ev1);
+// Chunked x' exchange: chunk k = class-A row blocks [b0, b1) of this rank + the slot-relative
+// pieces (offset, count) its rows complete; pieces are identical on every rank.
+struct XPiece {
+  uint64_t off, cnt;
+};
+struct XChunk {
+  uint32_t b0 = 0, b1 = 0;
+  std::vector<XPiece> pieces;
+};
+std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K);
 // After the exchange: combine p records -> next round's addthis / error / residual.
 int dev_round_finalize(DevGraph* g, int t, bool tracked, hipStream_t s);
 // Round-1 state (r^0 == 1): a = W0 / n_tot.

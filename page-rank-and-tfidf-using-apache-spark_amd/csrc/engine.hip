@@ -186,6 +186,7 @@ struct RowArgs {
   uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
   uint32_t dbg;              // PR_DBG timing experiments: 16 no LDS adds, 32 no epilogue, 64 no pieces
   double base, r0;           // damping base (0.15) and initial rank (1.0), or their /N_tot forms
+  uint32_t b0;               // first row block of this launch (the row launch may be chunked)
 };
 
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   __shared__ uint32_t pre[NSC + 1], st[NSC];
   __shared__ uint32_t wtot[4];
   __shared__ uint64_t lds[4][REC_WORDS];
-  const uint32_t b = blockIdx.x;
+  const uint32_t b = blockIdx.x + A.b0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < 4 * RB; i += BLOCK) (&acc[0][0])[i] = 0.0;
   for (int i = tid; i < 4 * REC_WORDS; i += BLOCK) (&lds[0][0])[i] = 0;
@@ -2017,8 +2018,7 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
 
 }  // namespace
 
-int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev0,
-                      hipEvent_t ev1) {
+int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   std::string* err = nullptr;
   const double* x_in = t == 1 ? (g->seeded ? g->x_seed : g->x_init) : g->xbuf[t & 1];
   StreamArgs S{};
@@ -2049,31 +2049,6 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
-  RowArgs A{};
-  A.T = g->runs;
-  A.partial = g->partial;
-  A.roff = g->roff;
-  A.dbg = static_cast<uint32_t>(g->tune.dbg);
-  A.NS = g->n_streams;
-  A.rb = g->row_rb;
-  A.nbH = g->row_nbH;
-  A.rbH = g->row_rbH;
-  A.lH = g->row_lH;
-  A.nbA = g->nb_rows_a;
-  A.lA = g->lA;
-  A.lrows = g->lrows;
-  A.meta = g->meta;
-  A.x_out = dev_x_out(g, t) + static_cast<uint64_t>(g->rank) * g->maxA;
-  A.r_old = t == 1 ? (g->seeded ? g->r_seed : nullptr) : g->r_loc[(t - 1) & 1];
-  A.base = g->base;
-  A.r0 = g->r0;
-  A.r_out = g->r_loc[t & 1];
-  A.st = g->state;
-  A.shards = g->shards;
-  A.p = static_cast<uint32_t>(g->p);
-  A.rank = static_cast<uint32_t>(g->rank);
-  A.sm = g->sm ? 1u : 0u;
-  A.SL = g->SL;
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
   if (g->ntask) launch_stream(g, S, s);
   if (stamps) {  // PR_STAMPS: per-phase time of the stream launch (diagnostics only)
@@ -2112,8 +2087,40 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
       prev_end = end_avg;
     }
   }
-  if (g->nb_rows) {
-    const dim3 gr(g->nb_rows), bl(BLOCK);
+  HIPTRY(hipGetLastError());
+  return PR_OK;
+}
+
+int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipStream_t s) {
+  std::string* err = nullptr;
+  RowArgs A{};
+  A.T = g->runs;
+  A.partial = g->partial;
+  A.roff = g->roff;
+  A.dbg = static_cast<uint32_t>(g->tune.dbg);
+  A.NS = g->n_streams;
+  A.rb = g->row_rb;
+  A.nbH = g->row_nbH;
+  A.rbH = g->row_rbH;
+  A.lH = g->row_lH;
+  A.nbA = g->nb_rows_a;
+  A.lA = g->lA;
+  A.lrows = g->lrows;
+  A.meta = g->meta;
+  A.x_out = dev_x_out(g, t) + static_cast<uint64_t>(g->rank) * g->maxA;
+  A.r_old = t == 1 ? (g->seeded ? g->r_seed : nullptr) : g->r_loc[(t - 1) & 1];
+  A.base = g->base;
+  A.r0 = g->r0;
+  A.r_out = g->r_loc[t & 1];
+  A.st = g->state;
+  A.shards = g->shards;
+  A.p = static_cast<uint32_t>(g->p);
+  A.rank = static_cast<uint32_t>(g->rank);
+  A.sm = g->sm ? 1u : 0u;
+  A.SL = g->SL;
+  A.b0 = b0;
+  if (b1 > b0) {
+    const dim3 gr(b1 - b0), bl(BLOCK);
     if (A.NS <= 512) {
       if (mode == 0) hipLaunchKernelGGL((spmv_rows<0, 512>), gr, bl, 0, s, A);
       else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1, 512>), gr, bl, 0, s, A);
@@ -2124,10 +2131,60 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
       else hipLaunchKernelGGL((spmv_rows<2, MAX_NS>), gr, bl, 0, s, A);
     }
   }
+  HIPTRY(hipGetLastError());
+  return PR_OK;
+}
+
+int dev_round_reduce(DevGraph* g, hipStream_t s, hipEvent_t ev1) {
+  std::string* err = nullptr;
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
   hipLaunchKernelGGL(reduce_shards, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local);
   HIPTRY(hipGetLastError());
   return PR_OK;
+}
+
+int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev0,
+                      hipEvent_t ev1) {
+  int rc = dev_round_stream(g, t, s, ev0);
+  if (!rc) rc = dev_round_rows(g, t, mode, 0, g->nb_rows, s);
+  if (!rc) rc = dev_round_reduce(g, s, ev1);
+  return rc;
+}
+
+// Exchange plan of the chunked x' exchange (p > 1): chunk k covers the slot positions
+// [P_{k-1}, P_k) of every slice sub-region of a rank's slot (the same on every rank), and the
+// class-A row blocks [b0, b1) that write them on this rank.
+std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K) {
+  std::vector<XChunk> out;
+  const uint32_t p = static_cast<uint32_t>(g->p);
+  const uint32_t nsub = g->sm ? NSLICE / p : 1u;          // sub-regions of a slot
+  const uint64_t SLr = g->sm ? g->SL : g->maxA;            // entries per sub-region
+  const uint32_t rows_per_pos = g->sm ? nsub : 1u;         // local rows per sub-region position
+  K = std::max(1, std::min<int>(K, static_cast<int>(std::max<uint64_t>(SLr / CHUNK, 1))));
+  auto block_row0 = [&](uint32_t b) -> uint64_t {
+    if (b < g->row_nbH) return static_cast<uint64_t>(b) * g->row_rbH;
+    return g->row_lH + static_cast<uint64_t>(b - g->row_nbH) * g->row_rb;
+  };
+  uint64_t prev = 0;
+  uint32_t bprev = 0;
+  for (int k = 0; k < K; ++k) {
+    uint64_t P = (k == K - 1) ? SLr : ((SLr * (k + 1)) / K) / CHUNK * CHUNK;
+    if (P < prev) P = prev;
+    // local rows below P map below P in every sub-region: l < P * rows_per_pos
+    const uint64_t Lrow = P * rows_per_pos;
+    uint32_t b1 = bprev;
+    if (k == K - 1) b1 = g->nb_rows_a;
+    else while (b1 < g->nb_rows_a && block_row0(b1) < Lrow) ++b1;
+    XChunk c;
+    c.b0 = bprev;
+    c.b1 = b1;
+    for (uint32_t sub = 0; sub < nsub; ++sub)
+      if (P > prev) c.pieces.push_back({sub * SLr + prev, P - prev});
+    out.push_back(c);
+    prev = P;
+    bprev = b1;
+  }
+  return out;
 }
 
 int dev_round_finalize(DevGraph* g, int t, bool tracked, hipStream_t s) {
