@@ -54,7 +54,9 @@ struct IterState {
 };
 
 struct Tuning {
-  uint32_t qh = 458752; // PR_QH: L2-hot segment length per slice after the LDS blocks (3.5 MiB)
+  uint32_t qh = 131072; // PR_QH: L2-hot segment length per slice after the LDS blocks (1 MiB;
+                        // 3.5 MiB before the dedicated L2 waves: 128 Ki entries measured best
+                        // with them, profiles/r02/)
   uint32_t rb = 1024;   // PR_RB: rows per row-launch block (64..1024)
   uint32_t rb_heavy = 256;  // PR_RBH: rows per heavy row-launch block
   uint32_t heavy_deg = 128; // PR_HDEG: rows with in-degree >= this get heavy blocks (0 = none)
@@ -68,7 +70,9 @@ struct Tuning {
   int dbg = 0;          // PR_DBG: timing-only experiments in the stream kernel (see StreamArgs)
   int stream_wg = 1;    // PR_STREAM_WG: stream workgroups per CU (1 with the LDS copy)
   int l2mode = 0;       // PR_L2MODE: 0 = L2 tasks interleaved with the LDS phases, 1 = last
-  int l2w = 0;          // PR_L2W: waves per stream workgroup dedicated to the L2 group
+  int l2w = 4;          // PR_L2W: waves per stream workgroup dedicated to the L2 group
+                        // (of 16; 0 = L2 tasks shared out over the LDS phases as in round 1;
+                        // 2/3/4/5/6/8 measured at scale 26, 3-4 best)
 };
 
 struct DevGraph {

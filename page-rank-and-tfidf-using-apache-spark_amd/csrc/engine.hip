@@ -522,7 +522,7 @@ __device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[
 // NT: 2 = non-temporal piece stores.  SPLIT: dedicated L2 waves (A.l2w).  STAMPS: PR_STAMPS
 // diagnostics.  The variants are separate instantiations so that the default one carries no
 // register cost for the others.
-template <int NT, bool SPLIT, bool STAMPS, int POL = 0>
+template <int NT, bool SPLIT, bool STAMPS>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
   const uint32_t j = blockIdx.x % NSLICE;
@@ -582,22 +582,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   auto fetch = [&](uint32_t tt, bool lds_task, uint32_t gtb, uint64_t gbs) {
     const uint64_t o = gbs + static_cast<uint64_t>(tt - gtb) * TASK + lane * EPL;
     // groups are padded to whole tasks: these loads never leave the stream buffers
-    if constexpr (POL != 0) {
-      // cache-policy experiment (PR_POL): column / flag words by buffer loads with aux = POL
-      // (2 nt, 16 sc1, 18 nt sc1, 3 sc0 nt) so the streams stop evicting gathered x lines
-      const uint64_t gb = gbs + static_cast<uint64_t>(tt - gtb) * TASK;
-      if (lds_task) {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint16_t*>(col16 + gb), static_cast<short>(0), 2 * TASK, 0x00020000);
-        cn[0] = __builtin_amdgcn_raw_buffer_load_b128(r, lane * 32, 0, POL);
-        cn[1] = __builtin_amdgcn_raw_buffer_load_b128(r, lane * 32 + 16, 0, POL);
-      } else {
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(col + gb), static_cast<short>(0), 4 * TASK, 0x00020000);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cn[q] = __builtin_amdgcn_raw_buffer_load_b128(r, lane * 64 + 16 * q, 0, POL);
-      }
-    } else if (lds_task) {
+    if (lds_task) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
       cn[0] = cp[0];
       cn[1] = cp[1];
@@ -1516,7 +1501,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   dev_free(g);
   Tuning& T = g->tune;
   // p >= 2: a 1.5 MiB L2-hot range (per-rank SpMV -3 % at p = 2 and 4, -2 % at p = 8)
-  const int qh_def = p >= 2 ? 196608 : static_cast<int>(T.qh);
+  const int qh_def = p >= 2 ? 196608 : static_cast<int>(T.qh);  // (p = 1: Tuning::qh)
   T.qh = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_QH", qh_def)));
   T.seg = static_cast<uint32_t>(std::max(CHUNK, env_int("PR_SEG", static_cast<int>(T.seg))));
   T.nt = env_int("PR_NT", T.nt);
@@ -1995,21 +1980,7 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
     attr_set = true;
   }
   const bool split = A.l2w && A.nlds, st = A.stamps != nullptr;
-  static const int pol = env_int("PR_POL", 0);
-  static bool pattr = false;
-  if (!pattr) {
-    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 2>),
-                          reinterpret_cast<const void*>(&spmv_stream<2, true, false, 16>),
-                          reinterpret_cast<const void*>(&spmv_stream<2, true, false, 18>),
-                          reinterpret_cast<const void*>(&spmv_stream<2, true, false, 3>)})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    pattr = true;
-  }
-  if (split && !st && pol == 2) hipLaunchKernelGGL((spmv_stream<2, true, false, 2>), gr, bl, lds, s, A);
-  else if (split && !st && pol == 16) hipLaunchKernelGGL((spmv_stream<2, true, false, 16>), gr, bl, lds, s, A);
-  else if (split && !st && pol == 18) hipLaunchKernelGGL((spmv_stream<2, true, false, 18>), gr, bl, lds, s, A);
-  else if (split && !st && pol == 3) hipLaunchKernelGGL((spmv_stream<2, true, false, 3>), gr, bl, lds, s, A);
-  else if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
+  if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
   else if (split && st) hipLaunchKernelGGL((spmv_stream<2, true, true>), gr, bl, lds, s, A);
   else if (split) hipLaunchKernelGGL((spmv_stream<2, true, false>), gr, bl, lds, s, A);
   else if (st) hipLaunchKernelGGL((spmv_stream<2, false, true>), gr, bl, lds, s, A);
