@@ -114,6 +114,13 @@ struct DevGraph {
   double* partial = nullptr;      // [n_pieces] per-piece partial sums
   uint16_t* roff = nullptr;       // [n_pieces] row of each piece, relative to its row block
   uint32_t* runs = nullptr;       // [(nb_rows+1) * n_streams] first piece of (row block, stream)
+  // row-launch maps (engine.hip RowArgs): non-empty runs per block, 64-piece line maps
+  uint32_t* nebase = nullptr;     // per block: start - pre of each non-empty run
+  uint32_t* ne_off = nullptr;     // [nb_rows + 1]
+  uint32_t* l_off = nullptr;      // [nb_rows + 1] first line of each block
+  uint32_t* btot = nullptr;       // [nb_rows] pieces per block
+  uint16_t* lfirst = nullptr;     // [lines] block-relative run of the line's first piece
+  uint64_t* lmask = nullptr;      // [lines] run starts inside the line
   uint32_t* meta = nullptr;
   uint32_t* perm = nullptr;       // internal -> original
   uint32_t* outdeg = nullptr;     // by original id

@@ -162,16 +162,24 @@ __device__ double sa_to_double_dev(const uint64_t* limb) {
 // Row launch: rows are cut into blocks of RB rows (class-A blocks, then class-B blocks).  For
 // every block and every stream k = (slice, segment), the block's pieces of stream k are one
 // contiguous run of the partial array (pieces are in stream order, rows ascending inside a
-// stream): T[block][k] = first piece of the run, T[block + 1][k] = one past it.  Each wave
-// adds a fixed quarter of the block's runs (concatenated in stream order) into its own LDS
-// accumulator; c[row] = (acc0 + acc1) + (acc2 + acc3).  Then PageRank.java's damping /
-// contribution epilogue.
+// stream).  The block's non-empty runs, concatenated in stream order, form its piece
+// sequence i = 0 .. tot-1; run q covers i in [pre_q, pre_q + len_q) and piece i of run q is
+// partial[nebase_q + i] (nebase_q = run start - pre_q).  The sequence is cut into 64-piece
+// LINES; for every line the build stores the run of its first piece (lfirst) and a 64-bit
+// mask of the positions where a new run starts (lmask), so lane l of a line finds its piece
+// as nebase[lfirst + popcount(lmask & bits 1..l)] + i: no search.  Each wave adds a fixed
+// quarter of the block's lines into its own LDS accumulator; c[row] = (acc0 + acc1) + (acc2 +
+// acc3).  Then PageRank.java's damping / contribution epilogue.
 constexpr int RB = 1024;           // rows per row-launch block
 constexpr int MAX_NS = 1024;       // streams (slices x segments) the row launch supports
-// (NSC = 512 or 1024 stream capacity: the small one keeps four workgroups per CU)
-constexpr int EPR = 8;             // pieces per lane per step (16 measured slower)
+constexpr int EPR = 8;             // lines per wave per step (one piece per lane per line)
 struct RowArgs {
-  const uint32_t* T;       // [(NB + 1) * NS] run starts
+  const uint32_t* nebase;  // [ne_off[NB]] per block: start - pre of each non-empty run
+  const uint32_t* ne_off;  // [NB + 1] first run of each block in nebase
+  const uint32_t* l_off;   // [NB + 1] first line of each block in lfirst / lmask
+  const uint32_t* tot;     // [NB] pieces of each block
+  const uint16_t* lfirst;  // [lines] run (block-relative) of each line's first piece
+  const uint64_t* lmask;   // [lines] bit j: piece j of the line starts a run (j >= 1)
   const double* partial;   // per-piece partial sums of this round
   const uint16_t* roff;    // per-piece row offset inside its block
   uint32_t NS, nbA, lA, lrows;
@@ -246,12 +254,10 @@ __device__ __forceinline__ void flush_records(const RowArgs& A, uint64_t (*lds)[
 
 // The row launch (PageRank.java:139-145 reduceByKey(Sum) + mapValues, and the inputs of
 // :113 and :125-134 for the next round).
-template <int MODE, int NSC>
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
-  constexpr int SPT = NSC / BLOCK;  // streams per thread in the run prefix
   __shared__ double acc[4][RB];
-  __shared__ uint32_t pre[NSC + 1], st[NSC];
-  __shared__ uint32_t wtot[4];
+  __shared__ uint32_t nb[MAX_NS];   // the block's non-empty runs: start - pre
   __shared__ uint64_t lds[4][REC_WORDS];
   const uint32_t b = blockIdx.x + A.b0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -275,99 +281,60 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     ro[q] = 0.0;
     if (MODE == 2 && row < rb1) ro[q] = A.r_old ? A.r_old[row] : A.r0;
   }
-  // run lengths of the block's streams -> exclusive prefix pre[] (SPT streams per thread)
-  const uint32_t NS = A.NS;
-  const uint32_t* T0 = A.T + static_cast<uint64_t>(b) * NS;
-  uint32_t len[SPT];
-  uint32_t inc = 0;
-#pragma unroll
-  for (int q = 0; q < SPT; ++q) {
-    const uint32_t k = SPT * tid + q;
-    len[q] = 0;
-    if (k < NS) {
-      st[k] = T0[k];
-      len[q] = T0[NS + k] - T0[k];
-    }
-    inc += len[q];
-  }
-  const uint32_t mine = inc;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(inc, d);
-    if (lane >= d) inc += y;
-  }
-  if (lane == 63) wtot[wv] = inc;
+  const uint32_t ne0 = A.ne_off[b], nne = A.ne_off[b + 1] - ne0;
+  for (uint32_t q = tid; q < nne; q += BLOCK) nb[q] = A.nebase[ne0 + q];
+  const uint32_t tot = A.tot[b];
+  const uint32_t L0 = A.l_off[b], nl = A.l_off[b + 1] - L0;
   __syncthreads();
-  uint32_t base = 0;
-  for (int i = 0; i < wv; ++i) base += wtot[i];
-  uint32_t ex = base + inc - mine;
-#pragma unroll
-  for (int q = 0; q < SPT; ++q) {
-    const uint32_t k = SPT * tid + q;
-    if (k < NS) pre[k] = ex;
-    ex += len[q];
-  }
-  if (tid == 0) pre[NS] = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-  __syncthreads();
-  // this wave's quarter of the concatenated runs, EPR consecutive pieces per lane per step
-  const uint32_t total = pre[NS];
-  const uint32_t lo = static_cast<uint32_t>(static_cast<uint64_t>(total) * wv / 4);
-  const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(total) * (wv + 1) / 4);
+  // this wave's quarter of the lines; a step = EPR lines, lane l takes piece l of each
+  const uint32_t lo = static_cast<uint32_t>(static_cast<uint64_t>(nl) * wv / 4);
+  const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(nl) * (wv + 1) / 4);
   double* aw = acc[wv];
-  uint32_t kw = 0;  // wave-uniform lower bound of the stream search
-  // lane l takes pieces pos + l + 64u: the lanes of one load cover 64 consecutive pieces (one
-  // coalesced 512-B read inside a long run).  Two-stage pipeline: the next step's loads are
-  // issued before this step's LDS adds.
-  auto locate = [&](uint32_t pos, uint32_t (&pc)[EPR]) {
-    const uint32_t i0 = pos + lane;
-    // stream of i0: last k with pre[k] <= i0 (empty streams share pre with the next one);
-    // galloping search from the wave's lower bound
-    uint32_t k = kw, stp = 1;
-    while (k + stp < NS && pre[k + stp] <= i0) {
-      k += stp;
-      stp <<= 1;
-    }
-    uint32_t kh = min(k + stp, NS) - 1;
-    while (k < kh) {
-      const uint32_t mid = (k + kh + 1) >> 1;
-      if (pre[mid] <= i0) k = mid; else kh = mid - 1;
-    }
-#pragma unroll
-    for (int u = 0; u < EPR; ++u) {
-      const uint32_t i = i0 + 64u * u;
-      while (k + 1 < NS && pre[k + 1] <= i) ++k;
-      pc[u] = i < hi ? st[k] + (i - pre[k]) : 0u;  // never address past the pieces
-    }
-    kw = __builtin_amdgcn_readfirstlane(k);  // lane 0's stream after this step (monotone)
-  };
+  const uint64_t lbits = (2ull << lane) - 2ull;  // bits 1 .. lane
   double va[EPR], vb[EPR], sink = 0.0;
-  uint32_t ra[EPR], rbuf[EPR], pc[EPR];
-  auto issue = [&](uint32_t pos, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
-    locate(pos, pc);
+  uint32_t ra[EPR], rbuf[EPR];
+  uint32_t fa[EPR];
+  uint64_t ma[EPR];
+  // line maps of a step (wave-uniform loads), fetched one step ahead of their use
+  auto maps = [&](uint32_t L) {
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
-      vv[u] = A.partial[pc[u]];
-      rr[u] = A.roff[pc[u]];
+      const uint32_t Lu = min(L + u, nl ? nl - 1 : 0u);
+      fa[u] = A.lfirst[L0 + Lu];
+      ma[u] = A.lmask[L0 + Lu];
     }
   };
-  auto add = [&](uint32_t pos, const double (&vv)[EPR], const uint32_t (&rr)[EPR]) {
+  auto issue = [&](uint32_t L, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
+#pragma unroll
+    for (int u = 0; u < EPR; ++u) {
+      const uint32_t i = (L + u) * 64u + static_cast<uint32_t>(lane);
+      const uint32_t q = fa[u] + static_cast<uint32_t>(__popcll(ma[u] & lbits));
+      const uint32_t pc = (L + u < hi && i < tot) ? nb[q] + i : 0u;  // never past the pieces
+      vv[u] = A.partial[pc];
+      rr[u] = A.roff[pc];
+    }
+    maps(L + EPR);
+  };
+  auto add = [&](uint32_t L, const double (&vv)[EPR], const uint32_t (&rr)[EPR]) {
     // LDS adds in lane order inside each instruction: a fixed order for a fixed layout
 #pragma unroll
     for (int u = 0; u < EPR; ++u)
-      if (pos + lane + 64u * u < hi) {
+      if (L + u < hi && (L + u) * 64u + static_cast<uint32_t>(lane) < tot) {
         if (A.dbg & 16u) sink += vv[u] + rr[u];
         else atomicAdd(&aw[rr[u]], vv[u]);
       }
   };
-  constexpr uint32_t STEP = 64 * EPR;
   const uint32_t hi_loop = (A.dbg & 64u) ? lo : hi;  // timing: no piece loads at all
-  if (lo < hi_loop) issue(lo, va, ra);
-  for (uint32_t pos = lo; pos < hi_loop; pos += 2 * STEP) {
-    const bool n1 = pos + STEP < hi, n2 = pos + 2 * STEP < hi;
-    if (n1) issue(pos + STEP, vb, rbuf);
-    add(pos, va, ra);
-    if (n2) issue(pos + 2 * STEP, va, ra);
-    if (n1) add(pos + STEP, vb, rbuf);
+  if (lo < hi_loop) {
+    maps(lo);
+    issue(lo, va, ra);
+  }
+  for (uint32_t L = lo; L < hi_loop; L += 2 * EPR) {
+    const bool n1 = L + EPR < hi, n2 = L + 2 * EPR < hi;
+    if (n1) issue(L + EPR, vb, rbuf);
+    add(L, va, ra);
+    if (n2) issue(L + 2 * EPR, va, ra);
+    if (n1) add(L + EPR, vb, rbuf);
   }
   if (A.dbg & 16u) aw[lane] = sink;
   __syncthreads();
@@ -1466,6 +1433,7 @@ int env_int(const char* name, int def) {
 void dev_free(DevGraph* g) {
   auto F = [](void* p) { if (p) (void)hipFree(p); };
   F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->roff); F(g->runs);
+  F(g->nebase); F(g->ne_off); F(g->l_off); F(g->btot); F(g->lfirst); F(g->lmask);
   F(g->d_gtask); F(g->d_gstart); F(g->d_gbase); F(g->col16);
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
@@ -1911,6 +1879,63 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
       }
     }
     HIPTRY(hipMemcpyAsync(g->runs, hT.data(), 4 * tn, hipMemcpyHostToDevice, s));
+    // row-launch maps (see RowArgs): per block the non-empty runs (start - pre), the piece
+    // count, and per 64-piece line the run of its first piece + the run-start mask
+    {
+      const uint32_t NB = RBk.NB;
+      std::vector<uint32_t> hne, hneoff(NB + 1), hloff(NB + 1), htot(NB);
+      std::vector<uint16_t> hlf;
+      std::vector<uint64_t> hlm;
+      std::vector<uint32_t> pre_q;  // per block: pre of each non-empty run
+      uint64_t lines = 0;
+      for (uint32_t bb = 0; bb < NB; ++bb) {
+        hneoff[bb] = static_cast<uint32_t>(hne.size());
+        hloff[bb] = static_cast<uint32_t>(lines);
+        pre_q.clear();
+        uint32_t pre = 0;
+        for (uint32_t k = 0; k < NSs; ++k) {
+          const uint32_t st0 = hT[static_cast<uint64_t>(bb) * NSs + k];
+          const uint32_t len = hT[static_cast<uint64_t>(bb + 1) * NSs + k] - st0;
+          if (!len) continue;
+          hne.push_back(st0 - pre);
+          pre_q.push_back(pre);
+          pre += len;
+        }
+        htot[bb] = pre;
+        const uint32_t nl = (pre + 63) / 64;
+        uint32_t q = 0;
+        for (uint32_t L = 0; L < nl; ++L) {
+          const uint32_t i0 = L * 64;
+          while (q + 1 < pre_q.size() && pre_q[q + 1] <= i0) ++q;
+          uint64_t m = 0;
+          for (uint32_t r = q + 1; r < pre_q.size() && pre_q[r] < i0 + 64; ++r) m |= 1ull << (pre_q[r] - i0);
+          hlf.push_back(static_cast<uint16_t>(q));
+          hlm.push_back(m);
+        }
+        lines += nl;
+        if (lines > 0xFFFFFFF0ull) {
+          if (err) *err = "too many row-launch lines";
+          return PR_E_ARG;
+        }
+      }
+      hneoff[NB] = static_cast<uint32_t>(hne.size());
+      hloff[NB] = static_cast<uint32_t>(lines);
+      TRY(dmalloc(&g->nebase, hne.size(), err));
+      TRY(dmalloc(&g->ne_off, NB + 1ull, err));
+      TRY(dmalloc(&g->l_off, NB + 1ull, err));
+      TRY(dmalloc(&g->btot, NB, err));
+      TRY(dmalloc(&g->lfirst, lines, err));
+      TRY(dmalloc(&g->lmask, lines, err));
+      if (!hne.empty()) HIPTRY(hipMemcpyAsync(g->nebase, hne.data(), 4 * hne.size(), hipMemcpyHostToDevice, s));
+      HIPTRY(hipMemcpyAsync(g->ne_off, hneoff.data(), 4ull * (NB + 1), hipMemcpyHostToDevice, s));
+      HIPTRY(hipMemcpyAsync(g->l_off, hloff.data(), 4ull * (NB + 1), hipMemcpyHostToDevice, s));
+      if (NB) HIPTRY(hipMemcpyAsync(g->btot, htot.data(), 4ull * NB, hipMemcpyHostToDevice, s));
+      if (lines) {
+        HIPTRY(hipMemcpyAsync(g->lfirst, hlf.data(), 2 * lines, hipMemcpyHostToDevice, s));
+        HIPTRY(hipMemcpyAsync(g->lmask, hlm.data(), 8 * lines, hipMemcpyHostToDevice, s));
+      }
+      HIPTRY(hipStreamSynchronize(s));
+    }
     HIPTRY(hipStreamSynchronize(s));
     (void)hipFree(prow);
     (void)hipFree(pstream);
@@ -2065,7 +2090,12 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
 int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipStream_t s) {
   std::string* err = nullptr;
   RowArgs A{};
-  A.T = g->runs;
+  A.nebase = g->nebase;
+  A.ne_off = g->ne_off;
+  A.l_off = g->l_off;
+  A.tot = g->btot;
+  A.lfirst = g->lfirst;
+  A.lmask = g->lmask;
   A.partial = g->partial;
   A.roff = g->roff;
   A.dbg = static_cast<uint32_t>(g->tune.dbg);
@@ -2092,15 +2122,9 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
   A.b0 = b0;
   if (b1 > b0) {
     const dim3 gr(b1 - b0), bl(BLOCK);
-    if (A.NS <= 512) {
-      if (mode == 0) hipLaunchKernelGGL((spmv_rows<0, 512>), gr, bl, 0, s, A);
-      else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1, 512>), gr, bl, 0, s, A);
-      else hipLaunchKernelGGL((spmv_rows<2, 512>), gr, bl, 0, s, A);
-    } else {
-      if (mode == 0) hipLaunchKernelGGL((spmv_rows<0, MAX_NS>), gr, bl, 0, s, A);
-      else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1, MAX_NS>), gr, bl, 0, s, A);
-      else hipLaunchKernelGGL((spmv_rows<2, MAX_NS>), gr, bl, 0, s, A);
-    }
+    if (mode == 0) hipLaunchKernelGGL((spmv_rows<0>), gr, bl, 0, s, A);
+    else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1>), gr, bl, 0, s, A);
+    else hipLaunchKernelGGL((spmv_rows<2>), gr, bl, 0, s, A);
   }
   HIPTRY(hipGetLastError());
   return PR_OK;
