@@ -655,51 +655,46 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     const int C = wave_incl_scan(cnt, lane);
     const uint32_t first = static_cast<uint32_t>(C - cnt);  // task-relative index of the lane's first start
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(C, 63));  // pieces of the task
-    // one pass over the lane's edges: the head (edges before its first start), the open piece,
-    // and pv[k] = the piece that closes just before edge k (static slots: no scratch)
-    double run = 0.0, head = 0.0;
+    // one pass over the lane's edges: pv[k] = the running sum just before edge k (for a start
+    // bit k that is the piece closing before k; for the lane's first start it is the head,
+    // the edges before it), run = the open piece at the lane's end.  Same adds, same order as
+    // a plain left-to-right sum per piece.
+    double run = 0.0;
     double pv[EPL];
-    {
-      bool ih = (b & 1u) == 0u;
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        pv[k] = 0.0;
-        if ((b >> k) & 1u) {
-          if (k > 0) {
-            if (ih) head = run;
-            else pv[k] = run;
-          }
-          ih = false;
-          run = 0.0;
-        }
-        run += v[k];
-      }
+    for (int k = 0; k < EPL; ++k) {
+      pv[k] = run;
+      const double t = run + v[k];
+      run = ((b >> k) & 1u) ? v[k] : t;
     }
-    // slot k holds a middle piece when edge k starts one and it is not the head's end
-    const uint32_t k0 = b ? static_cast<uint32_t>(__builtin_ctz(b)) : 32u;
-    const uint32_t mids = (b & ~1u) & ~((b & 1u) ? 0u : (1u << k0));
     // segmented inclusive scan of the open piece over lanes (flag: lane holds a start)
     const double S = wave_seg_scan(run, b != 0u ? 1 : 0, lane);
     const double carry = dpp_d<DPP_WAVE_SHR1>(S);
     const uint32_t bn = static_cast<uint32_t>(dpp_i<DPP_WAVE_SHL1>(static_cast<int>(b)));
     const bool closes = lane == 63 || (bn & 1u) != 0u;  // next edge starts a piece
     // Pieces go to the wave's LDS staging window (STG pieces at a time) and leave it as
-    // contiguous 512-byte stores: one L2 request per line instead of one per piece.
+    // contiguous 512-byte stores: one L2 request per line instead of one per piece.  Start
+    // bit k >= 1 closes the piece with index first - 1 + (starts before k, bit 0 included).
     for (uint32_t w0 = 0; w0 < total; w0 += STG) {
       const uint32_t wn = min(total - w0, static_cast<uint32_t>(STG));
-      auto put = [&](uint32_t r, double val) {
-        if (r - w0 < wn) stg[r - w0] = val;
-      };
       if (first + cnt > w0 && first < w0 + wn + 1u) {
+        // window slot of the next closing piece: piece first - 1 closes at the lane's first
+        // start k >= 1 (when edge 0 starts a piece, that earlier piece closed in lane - 1)
+        uint32_t idx = first - 1u + (b & 1u) - w0;
 #pragma unroll
-        for (int k = 1; k < EPL; ++k)
-          if ((mids >> k) & 1u)  // piece index: first - 1 + starts before edge k
-            put(first - 1u + static_cast<uint32_t>(__popc(b & ((1u << k) - 1u))), pv[k]);
+        for (int k = 1; k < EPL; ++k) {
+          const uint32_t bit = (b >> k) & 1u;
+          if (bit && idx < wn) stg[idx] = pv[k];
+          idx += bit;
+        }
+        // the head piece (closing at the lane's first start k0 > 0) also holds the pieces
+        // open in earlier lanes: carry + head, one add, fixed up in place (same lane wrote it)
+        const uint32_t hs = first - 1u - w0;
+        if (b != 0u && !(b & 1u) && hs < wn) stg[hs] = carry + stg[hs];
         if (b == 0u) {
-          if (closes) put(first - 1u, S);            // lane inside a longer piece
-        } else {
-          if (!(b & 1u)) put(first - 1u, carry + head);
-          if (closes) put(static_cast<uint32_t>(C) - 1u, run);  // the lane's last piece
+          if (closes && first - 1u - w0 < wn) stg[first - 1u - w0] = S;  // inside a longer piece
+        } else if (closes && static_cast<uint32_t>(C) - 1u - w0 < wn) {
+          stg[static_cast<uint32_t>(C) - 1u - w0] = run;  // the lane's last piece
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
