@@ -59,6 +59,7 @@ struct Tuning {
                         // with them, profiles/r02/)
   uint32_t rb = 1024;   // PR_RB: rows per row-launch block (64..1024)
   uint32_t rb_heavy = 256;  // PR_RBH: rows per heavy row-launch block
+  uint32_t rxg = 16;     // PR_RXG: consecutive row-launch blocks per XCD (1 = round-robin)
   uint32_t heavy_deg = 128; // PR_HDEG: rows with in-degree >= this get heavy blocks (0 = none)
   int nlds = 18;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)

@@ -195,6 +195,7 @@ struct RowArgs {
   uint32_t dbg;              // PR_DBG timing experiments: 16 no LDS adds, 32 no epilogue, 64 no pieces
   double base, r0;           // damping base (0.15) and initial rank (1.0), or their /N_tot forms
   uint32_t b0;               // first row block of this launch (the row launch may be chunked)
+  uint32_t xg, xfull;        // XCD groups: xg consecutive blocks per XCD in the first xfull
 };
 
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
@@ -259,7 +260,14 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   __shared__ double acc[4][RB];
   __shared__ uint32_t nb[MAX_NS];   // the block's non-empty runs: start - pre
   __shared__ uint64_t lds[4][REC_WORDS];
-  const uint32_t b = blockIdx.x + A.b0;
+  // workgroups go round-robin over the 8 XCDs: give each XCD runs of xg consecutive blocks,
+  // so the piece lines that two neighbouring blocks' runs share are fetched into one L2
+  uint32_t bl = blockIdx.x;
+  if (bl < A.xfull) {
+    const uint32_t span = NSLICE * A.xg, r = bl % span;
+    bl = (bl - r) + (r % NSLICE) * A.xg + r / NSLICE;
+  }
+  const uint32_t b = bl + A.b0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int i = tid; i < 4 * RB; i += BLOCK) (&acc[0][0])[i] = 0.0;
   for (int i = tid; i < 4 * REC_WORDS; i += BLOCK) (&lds[0][0])[i] = 0;
@@ -1473,6 +1481,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.rb_heavy = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RBH", static_cast<int>(T.rb_heavy)))));
   T.heavy_deg = static_cast<uint32_t>(std::max(0, env_int("PR_HDEG", static_cast<int>(T.heavy_deg))));
   T.rb = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RB", static_cast<int>(T.rb)))));
+  T.rxg = static_cast<uint32_t>(std::max(1, std::min(4096, env_int("PR_RXG", static_cast<int>(T.rxg)))));
   // a rank's share of each (slice, LDS block) phase shrinks with p while the per-phase cost
   // (block fill, phase tail) stays: fewer blocks per slice at p > 1 (measured per-rank SpMV
   // at scale 26: p = 2 best at 15, p = 4 and 8 at 12; profiles/r01/multirank/)
@@ -2115,6 +2124,8 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
   A.sm = g->sm ? 1u : 0u;
   A.SL = g->SL;
   A.b0 = b0;
+  A.xg = std::max(1u, g->tune.rxg);
+  A.xfull = (b1 - b0) / (NSLICE * A.xg) * (NSLICE * A.xg);
   if (b1 > b0) {
     const dim3 gr(b1 - b0), bl(BLOCK);
     if (mode == 0) hipLaunchKernelGGL((spmv_rows<0>), gr, bl, 0, s, A);
