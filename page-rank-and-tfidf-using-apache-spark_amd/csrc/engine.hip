@@ -1480,7 +1480,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.dbg = env_int("PR_DBG", 0);
   T.rb_heavy = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RBH", static_cast<int>(T.rb_heavy)))));
   T.heavy_deg = static_cast<uint32_t>(std::max(0, env_int("PR_HDEG", static_cast<int>(T.heavy_deg))));
-  T.rb = static_cast<uint32_t>(std::max(64, std::min(2 * RB, env_int("PR_RB", static_cast<int>(T.rb)))));
+  T.rb = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RB", static_cast<int>(T.rb)))));
   T.rxg = static_cast<uint32_t>(std::max(1, std::min(4096, env_int("PR_RXG", static_cast<int>(T.rxg)))));
   // a rank's share of each (slice, LDS block) phase shrinks with p while the per-phase cost
   // (block fill, phase tail) stays: fewer blocks per slice at p > 1 (measured per-rank SpMV
@@ -2131,11 +2131,7 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
     // blocks of <= 512 rows (and heavy blocks) fit the half-size accumulators: more
     // workgroups per CU
     const bool half = A.rb <= RB / 2 && (A.nbH == 0 || A.rbH <= RB / 2);
-    if (A.rb > RB) {
-      if (mode == 0) hipLaunchKernelGGL((spmv_rows<0, 2 * RB>), gr, bl, 0, s, A);
-      else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1, 2 * RB>), gr, bl, 0, s, A);
-      else hipLaunchKernelGGL((spmv_rows<2, 2 * RB>), gr, bl, 0, s, A);
-    } else if (half) {
+    if (half) {
       if (mode == 0) hipLaunchKernelGGL((spmv_rows<0, RB / 2>), gr, bl, 0, s, A);
       else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1, RB / 2>), gr, bl, 0, s, A);
       else hipLaunchKernelGGL((spmv_rows<2, RB / 2>), gr, bl, 0, s, A);
