@@ -255,9 +255,9 @@ __device__ __forceinline__ void flush_records(const RowArgs& A, uint64_t (*lds)[
 
 // The row launch (PageRank.java:139-145 reduceByKey(Sum) + mapValues, and the inputs of
 // :113 and :125-134 for the next round).
-template <int MODE, int RBT = RB>
+template <int MODE>
 __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
-  __shared__ double acc[4][RBT];
+  __shared__ double acc[4][RB];
   __shared__ uint32_t nb[MAX_NS];   // the block's non-empty runs: start - pre
   __shared__ uint64_t lds[4][REC_WORDS];
   // workgroups go round-robin over the 8 XCDs: give each XCD runs of xg consecutive blocks,
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   }
   const uint32_t b = bl + A.b0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < 4 * RBT; i += BLOCK) (&acc[0][0])[i] = 0.0;
+  for (int i = tid; i < 4 * RB; i += BLOCK) (&acc[0][0])[i] = 0.0;
   for (int i = tid; i < 4 * REC_WORDS; i += BLOCK) (&lds[0][0])[i] = 0;
   // the block's rows; their epilogue inputs are loaded now, used after the piece loop
   const bool clsB = b >= A.nbA;
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * A.rb
                             : (heavy ? b * A.rbH : A.lH + (b - A.nbH) * A.rb);
   const uint32_t rb1 = min(rb0 + (heavy ? A.rbH : A.rb), clsB ? A.lrows : A.lA);
-  constexpr int RPT = RBT / BLOCK;  // rows per thread
+  constexpr int RPT = RB / BLOCK;  // rows per thread
   uint32_t mt[RPT];
   double ro[RPT];
 #pragma unroll
@@ -2128,14 +2128,7 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
   A.xfull = (b1 - b0) / (NSLICE * A.xg) * (NSLICE * A.xg);
   if (b1 > b0) {
     const dim3 gr(b1 - b0), bl(BLOCK);
-    // blocks of <= 512 rows (and heavy blocks) fit the half-size accumulators: more
-    // workgroups per CU
-    const bool half = A.rb <= RB / 2 && (A.nbH == 0 || A.rbH <= RB / 2);
-    if (half) {
-      if (mode == 0) hipLaunchKernelGGL((spmv_rows<0, RB / 2>), gr, bl, 0, s, A);
-      else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1, RB / 2>), gr, bl, 0, s, A);
-      else hipLaunchKernelGGL((spmv_rows<2, RB / 2>), gr, bl, 0, s, A);
-    } else if (mode == 0) hipLaunchKernelGGL((spmv_rows<0>), gr, bl, 0, s, A);
+    if (mode == 0) hipLaunchKernelGGL((spmv_rows<0>), gr, bl, 0, s, A);
     else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1>), gr, bl, 0, s, A);
     else hipLaunchKernelGGL((spmv_rows<2>), gr, bl, 0, s, A);
   }
