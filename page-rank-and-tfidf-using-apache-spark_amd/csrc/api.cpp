@@ -483,6 +483,7 @@ int pr_comm_init_local(pr_ctx** ctxs, int32_t n) {
 }
 
 int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_stats* st) {
+  prmi::Span span("prmi:run_group");
   if (!ctxs || n < 1) return PR_E_ARG;
   pr_ctx* c0 = ctxs[0];
   for (int i = 0; i < n; ++i) {
@@ -544,6 +545,7 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
     if (plans[i].size() != plans[0].size()) return fail(c0, PR_E_ARG, "local group: exchange plans differ");
   for (int t = 1; t <= iterations; ++t) {
     const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
+    prmi::Span round("prmi:round");
     // the schedule of pr_run's chunked exchange, with device copies for ncclSend/Recv: each
     // member's rows run in chunks; member q's comm stream copies chunk k of every peer's
     // slot as soon as that peer's chunk event fires, then the records, then finalize
@@ -659,6 +661,7 @@ int pr_ext_begin(pr_ctx* c, int32_t iterations, double tol, uint64_t* bytes_per_
 }
 
 int pr_ext_round(pr_ctx* c, int32_t t, void* send) {
+  prmi::Span span("prmi:ext_round");
   int rc = need_device(c);
   if (rc) return rc;
   if (!c->external || t != c->ext_done + 1 || t > c->ext_iters || !send)
@@ -677,6 +680,7 @@ int pr_ext_round(pr_ctx* c, int32_t t, void* send) {
 }
 
 int pr_ext_complete(pr_ctx* c, int32_t t, const void* recv_all, int32_t* stop) {
+  prmi::Span span("prmi:ext_complete");
   int rc = need_device(c);
   if (rc) return rc;
   if (!c->external || t != c->ext_done + 1 || !recv_all)
@@ -725,6 +729,7 @@ int pr_ext_end(pr_ctx* c, pr_stats* st) {
 }
 
 int pr_ingest_buffers(pr_ctx* c, const char* arcs, size_t alen, const char* map, size_t mlen) {
+  prmi::Span span("prmi:ingest");
   if (!c || (!arcs && alen) || (!map && mlen)) return fail(c, PR_E_ARG, "bad buffers");
   int rc = need_comm(c);
   if (rc) return rc;
@@ -873,6 +878,7 @@ int pr_graph_get_info(pr_ctx* c, pr_graph_info* o) {
 }
 
 int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
+  prmi::Span span("prmi:run");
   int rc = need_device(c);
   if (rc) return rc;
   rc = need_graph(c);
@@ -924,6 +930,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   }
   for (int t = 1; t <= iterations; ++t) {
     const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
+    prmi::Span round("prmi:round");
     hipEvent_t e0 = t <= nk ? c->kev[2 * (t - 1)] : nullptr;
     hipEvent_t e1 = t <= nk ? c->kev[2 * (t - 1) + 1] : nullptr;
     if (p == 1) {
@@ -1367,6 +1374,7 @@ int tf_rows(pr_ctx* c, const char* word, size_t wlen, std::vector<TfRow>* rows) 
 }  // namespace
 
 int pr_tfidf_ingest_buffer(pr_ctx* c, const char* data, size_t len) {
+  prmi::Span span("prmi:tfidf");
   if (!c || (!data && len)) return c ? fail(c, PR_E_ARG, "bad buffer") : PR_E_ARG;
   int rc = need_device(c);
   if (rc) return rc;

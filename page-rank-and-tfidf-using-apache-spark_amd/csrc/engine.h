@@ -21,6 +21,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdint>
 #include <string>
@@ -29,6 +30,24 @@
 #include "host_graph.h"
 
 namespace prmi {
+
+// roctx ranges (rocprofv3 --marker-trace): host-side spans of the build phases, ingest, runs
+// and rounds.  Scope = one push/pop; next() closes the previous phase and opens another.
+class Span {
+ public:
+  explicit Span(const char* name) { roctxRangePushA(name); depth_ = 1; }
+  ~Span() { while (depth_-- > 0) roctxRangePop(); }
+  void next(const char* phase) {
+    if (depth_ > 1) { roctxRangePop(); --depth_; }
+    roctxRangePushA(phase);
+    ++depth_;
+  }
+  Span(const Span&) = delete;
+  Span& operator=(const Span&) = delete;
+
+ private:
+  int depth_ = 0;
+};
 
 constexpr int SA_LIMBS = 10;       // exact accumulator: 10 x 32-bit chunks, unit 2^-96
 constexpr int SA_BASE_EXP = -96;

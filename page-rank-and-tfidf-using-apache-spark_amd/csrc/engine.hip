@@ -1467,6 +1467,7 @@ uint32_t owned_rows(uint32_t cnt, uint32_t p, uint32_t j) {
 }  // namespace
 
 int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err) {
+  Span span("prmi:build");
   auto t0 = std::chrono::steady_clock::now();
   const int p = g->p, rank = g->rank;
   dev_free(g);
@@ -1512,6 +1513,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   }
   Temp tmp;
 
+  span.next("prmi:build:raw keys");
   // ---- raw keys (dst << nb | src) ------------------------------------------------------
   uint64_t *kA = nullptr, *kB = nullptr;
   TRY(dmalloc(&kA, m, err));
@@ -1539,6 +1541,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   }
   HIPTRY(hipGetLastError());
 
+  span.next("prmi:build:distinct");
   // ---- distinct() (PageRank.java:42): sort + unique -------------------------------------
   uint64_t nnz = 0;
   uint64_t* uniq = nullptr;  // points into kA or kB
@@ -1563,6 +1566,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   }
   g->nnz = nnz;
 
+  span.next("prmi:build:degrees + vertex order");
   // ---- degrees + digest + dangling weights + vertex order -------------------------------
   TRY(dmalloc(&g->outdeg, n, err));
   TRY(dmalloc(&g->indeg, n, err));
@@ -1665,6 +1669,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   g->lA = owned_rows(g->nA, P, RK);
   const Layout L = layout_of(g);
 
+  span.next("prmi:build:x vectors + row data");
   // ---- x vectors ------------------------------------------------------------------------
   TRY(dmalloc(&g->x_init, g->X, err));
   TRY(dmalloc(&g->xbuf[0], g->X, err));
@@ -1717,6 +1722,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   }
   const uint32_t NG = NSLICE * (G.nlds + 1);
 
+  span.next("prmi:build:stream keys + sort");
   // ---- local edges: stream keys, stable radix sort -------------------------------------------
   uint64_t* lk_in = uniq == kA ? kB : kA;  // free buffer
   unsigned long long* d_cnt = nullptr;     // [0] local edges [1] unused [2..] group starts
@@ -1770,6 +1776,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   HIPTRY(hipMemcpyAsync(g->d_gtask, g->gtask.data(), 4ull * (NG + 1), hipMemcpyHostToDevice, s));
   HIPTRY(hipMemcpyAsync(g->d_gstart, g->gstart.data(), 8ull * (NG + 1), hipMemcpyHostToDevice, s));
 
+  span.next("prmi:build:stream arrays");
   // ---- stream arrays: columns (u16 for LDS groups, u32 for the L2 group), flags, pieces --------
   {
     g->gbase.assign(NG + 1, 0);
@@ -1818,6 +1825,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     for (unsigned long long v : hp) g->n_pairs += v;
   }
   const uint64_t NP = g->n_pieces;
+  span.next("prmi:build:row maps");
   // ---- row launch: row blocks, per-piece row offsets, run table ------------------------------
   RowBlocks RBk{};
   const uint32_t rbs = T.rb;
@@ -1955,6 +1963,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   // PR_DBG experiments may skip the partial stores: keep every rank defined
   if (T.dbg && NP) hipLaunchKernelGGL(k_fill_f64, dim3(grid_loop(NP)), dim3(BLOCK), 0, s, g->partial, NP, 1.0);
 
+  span.next("prmi:build:iteration buffers");
   // ---- iteration buffers ----------------------------------------------------------------
   TRY(dmalloc(&g->r_loc[0], lrows, err));
   TRY(dmalloc(&g->r_loc[1], lrows, err));

@@ -92,3 +92,12 @@ def test_missing_library_fails_loudly(engine_mod, monkeypatch, tmp_path):
     monkeypatch.setattr(P, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(RuntimeError, match="not built"):
         P.Engine()
+
+
+def test_library_emits_roctx_ranges(engine_mod):
+    """Build phases, ingest, runs and rounds are roctx ranges (rocprofv3 --marker-trace;
+    profiles/r02/marker_stats.csv holds a traced bench run)."""
+    out = subprocess.run(["nm", "-D", engine_mod.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    und = {ln.split()[-1] for ln in out.splitlines() if " U " in ln}
+    assert {"roctxRangePushA", "roctxRangePop"} <= und
