@@ -125,6 +125,21 @@ int build_device(pr_ctx* c, const prmi::BuildInput& in0) {
             c->dg.lrows, (unsigned long long)c->dg.lnnz, c->dg.nseg,
             (unsigned long long)c->dg.n_pairs, (unsigned long long)c->dg.n_pieces,
             c->dg.ntask, (size_t)c->dg.n_streams, c->dg.nb_rows);
+  if ((c->opts.flags & PR_F_VERBOSE) || getenv("PR_VERBOSE")) {
+    // algorithmic HBM bytes of one round per array (each array touched once)
+    const prmi::DevGraph& g = c->dg;
+    const uint64_t xlds = 8ull * prmi::NSLICE * g.nlds * g.hot_h;
+    auto U = [](uint64_t v) { return static_cast<unsigned long long>(v); };
+    fprintf(stderr, "[prmi355x] rank %d round bytes: col16=%llu col32=%llu bits=%llu task_piece=%llu "
+            "x_lds=%llu x_rest=%llu piece_w=%llu piece_r=%llu roff=%llu row_maps=%llu meta=%llu "
+            "x_out=%llu n_col16=%llu n_col32=%llu lines=%llu runs=%llu\n",
+            c->opts.rank, U(2ull * g.n_col16), U(4ull * g.n_col32), U(g.stream_len / 8),
+            U(4ull * (g.ntask + 1ull)), U(std::min<uint64_t>(xlds, 8ull * g.X)),
+            U(8ull * g.X - std::min<uint64_t>(xlds, 8ull * g.X)), U(8ull * g.n_pieces),
+            U(8ull * g.n_pieces), U(2ull * g.n_pieces),
+            U(10ull * g.n_lines + 4ull * g.n_runs + 12ull * g.nb_rows), U(4ull * g.lrows),
+            U(8ull * g.lA), U(g.n_col16), U(g.n_col32), U(g.n_lines), U(g.n_runs));
+  }
   return PR_OK;
 }
 

@@ -125,6 +125,7 @@ struct DevGraph {
   uint32_t nlds = 0, hot_h = 0;   // LDS blocks per slice and their length (x entries)
   uint32_t nseg = 0;              // segments per slice (LDS blocks + L2-hot + cold)
   uint64_t n_pieces = 0, n_pairs = 0;
+  uint64_t n_lines = 0, n_runs = 0;  // row-launch 64-piece lines, non-empty (block, stream) runs
   uint64_t stream_len = 0;        // padded length of col (multiple of TASK)
   // device arrays
   uint32_t* col = nullptr;        // [n_col32] L2-group edges: x position of the source

@@ -384,7 +384,8 @@ struct StreamArgs {
   uint32_t hot_base[NSLICE]; // x position of each slice region's start
   uint32_t nlds, H;          // LDS blocks per slice, entries per block
   uint32_t colmask;          // PR_COLMASK (timing experiments only)
-  uint32_t dbg;              // PR_DBG timing experiments: 1 no stores, 2 no gathers, 4 no starts
+  uint32_t dbg;              // PR_DBG timing experiments: 1 no stores, 2 no L2 gathers, 4 no
+                             // starts, 8 no LDS gathers
   uint32_t x_bytes;          // bytes of x (< 2^31: the buffer-load range check drops LDS lanes
                              // and PAD_COL padding)
   uint32_t l2mode;           // PR_L2MODE: 0 = L2 tasks interleaved 1/nlds per LDS phase,
@@ -635,10 +636,16 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       double v[EPL];
       if (lds_task) {
         // every source of an LDS-group task is inside the block (padding reads the zero slot)
+        if (A.dbg & 8u) {  // timing: no LDS gathers
 #pragma unroll
-        for (int k = 0; k < EPL; ++k) {
-          const uint32_t wd = cv[k >> 3][(k >> 1) & 3];
-          v[k] = hot[(k & 1) ? (wd >> 16) : (wd & 0xFFFFu)];
+          for (int k = 0; k < EPL; ++k)
+            v[k] = __longlong_as_double(static_cast<long long>(cv[k >> 3][(k >> 1) & 3] & 0x3FFFu));
+        } else {
+#pragma unroll
+          for (int k = 0; k < EPL; ++k) {
+            const uint32_t wd = cv[k >> 3][(k >> 1) & 3];
+            v[k] = hot[(k & 1) ? (wd >> 16) : (wd & 0xFFFFu)];
+          }
         }
       } else {
         // sixteen buffer gathers issued back to back; PAD_COL lanes fall outside the buffer
@@ -1932,6 +1939,8 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
       }
       hneoff[NB] = static_cast<uint32_t>(hne.size());
       hloff[NB] = static_cast<uint32_t>(lines);
+      g->n_lines = lines;
+      g->n_runs = hne.size();
       TRY(dmalloc(&g->nebase, hne.size(), err));
       TRY(dmalloc(&g->ne_off, NB + 1ull, err));
       TRY(dmalloc(&g->l_off, NB + 1ull, err));
