@@ -9,7 +9,7 @@ PARITY STATUS: *parity unpinned*.  The reference (``/root/reference/PageRank.jav
 be run in this image (no JVM, no Spark -- SURVEY.md section 8c).  This restatement is pinned
 instead by (a) the hand-checked known-answer tests of SURVEY.md Appendix B and (b) bit-exact
 agreement with the independent dense C restatement ``oracle/pagerank_oracle.c`` on
-thousands of random graphs (``tests/test_oracle_equivalence.py``).
+thousands of random graphs (``tests/test_oracle.py``).
 
 What it does: replays every Spark operator of ``PageRank.main`` (PageRank.java:21-204) with
 Python dicts / lists, in program order, so that the behaviour -- including the reference's

@@ -1226,6 +1226,60 @@ __global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, uint3
   }
 }
 
+// PR_PIECE_STATS (build-time report): pieces and edges by row in-degree bin (bin b holds
+// in-degrees [2^b, 2^(b+1))) and by segment kind (0 LDS block, 1 L2-hot, 2 cold)
+constexpr int PS_BINS = 24;
+__device__ __forceinline__ int ps_bin(uint32_t d) { return d ? min(31 - __clz(d), PS_BINS - 1) : 0; }
+__device__ __forceinline__ uint32_t ps_kind(uint32_t seg, uint32_t nlds) {
+  return seg < nlds ? 0u : (seg == nlds ? 1u : 2u);
+}
+__global__ void k_ps_edges(const uint64_t* key, uint64_t n, StreamGeo G, uint32_t* rowcnt) {
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    if (e < n) atomicAdd(&rowcnt[static_cast<uint32_t>(key[e] >> G.qb) & ((1u << G.rb) - 1u)], 1u);
+  }
+}
+// hist[bin][kind][0 pieces | 1 edges], rows[bin]
+__global__ void k_ps_pieces(const uint32_t* prow, const uint32_t* pstream, uint64_t np,
+                            uint32_t nseg, uint32_t nlds, const uint32_t* rowcnt,
+                            unsigned long long* hist) {
+  __shared__ unsigned long long h[PS_BINS * 3];
+  for (int i = threadIdx.x; i < PS_BINS * 3; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  PRMI_BLOCK_LOOP(np) {
+    const uint64_t i = blk_ * blockDim.x + threadIdx.x;
+    if (i < np)
+      atomicAdd(&h[ps_bin(rowcnt[prow[i]]) * 3 + ps_kind(pstream[i] % nseg, nlds)], 1ull);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < PS_BINS * 3; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[(i / 3) * 6 + (i % 3) * 2], h[i]);
+}
+__global__ void k_ps_edge_kinds(const uint64_t* key, uint64_t n, StreamGeo G, uint32_t nlds,
+                                const uint32_t* rowcnt, unsigned long long* hist,
+                                unsigned long long* rows) {
+  __shared__ unsigned long long h[PS_BINS * 3];
+  for (int i = threadIdx.x; i < PS_BINS * 3; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  PRMI_BLOCK_LOOP(n) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    if (e < n) {
+      const uint64_t k = key[e];
+      const uint32_t l = static_cast<uint32_t>(k >> G.qb) & ((1u << G.rb) - 1u);
+      const uint32_t seg = static_cast<uint32_t>(k >> (G.rb + G.qb)) & ((1u << G.sgb) - 1u);
+      atomicAdd(&h[ps_bin(rowcnt[l]) * 3 + ps_kind(seg, nlds)], 1ull);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < PS_BINS * 3; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[(i / 3) * 6 + (i % 3) * 2 + 1], h[i]);
+  (void)rows;
+}
+__global__ void k_ps_rows(const uint32_t* rowcnt, uint32_t nrows, unsigned long long* rows) {
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l < nrows && rowcnt[l]) atomicAdd(&rows[ps_bin(rowcnt[l])], 1ull);
+}
+
 // row blocks of the row launch: class-A rows in blocks of RB, then class-B rows
 struct RowBlocks {
   uint32_t lA, nbA, NB, NS, rb;
@@ -1878,6 +1932,38 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     HIPTRY(hipMemsetAsync(sst, 0xFF, 4ull * RBk.NS, s));
     if (lnnz) hipLaunchKernelGGL(k_piece_rows, dim3(grid_loop(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, g->nseg, g->d_gstart, g->d_gtask, bits32, g->task_piece, prow, pstream);
     if (NP) hipLaunchKernelGGL(k_runs, dim3(grid_loop(NP)), dim3(BLOCK), 0, s, prow, pstream, NP, RBk, g->roff, g->runs, sst);
+    if (env_int("PR_PIECE_STATS", 0) && lrows) {
+      uint32_t* rowcnt = nullptr;
+      unsigned long long *hist = nullptr, *rows = nullptr;
+      TRY(dmalloc(&rowcnt, lrows, err));
+      TRY(dmalloc(&hist, PS_BINS * 6, err));
+      TRY(dmalloc(&rows, PS_BINS, err));
+      HIPTRY(hipMemsetAsync(rowcnt, 0, 4ull * lrows, s));
+      HIPTRY(hipMemsetAsync(hist, 0, 8ull * PS_BINS * 6, s));
+      HIPTRY(hipMemsetAsync(rows, 0, 8ull * PS_BINS, s));
+      if (lnnz) hipLaunchKernelGGL(k_ps_edges, dim3(grid_loop(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, rowcnt);
+      if (NP) hipLaunchKernelGGL(k_ps_pieces, dim3(grid_loop(NP)), dim3(BLOCK), 0, s, prow, pstream, NP, g->nseg, g->nlds, rowcnt, hist);
+      if (lnnz) hipLaunchKernelGGL(k_ps_edge_kinds, dim3(grid_loop(lnnz)), dim3(BLOCK), 0, s, lk, lnnz, G, g->nlds, rowcnt, hist, rows);
+      hipLaunchKernelGGL(k_ps_rows, dim3(grid_for(lrows)), dim3(BLOCK), 0, s, rowcnt, lrows, rows);
+      std::vector<unsigned long long> hh(PS_BINS * 6), hr(PS_BINS);
+      HIPTRY(hipMemcpyAsync(hh.data(), hist, 8ull * PS_BINS * 6, hipMemcpyDeviceToHost, s));
+      HIPTRY(hipMemcpyAsync(hr.data(), rows, 8ull * PS_BINS, hipMemcpyDeviceToHost, s));
+      HIPTRY(hipStreamSynchronize(s));
+      (void)hipFree(rowcnt);
+      (void)hipFree(hist);
+      (void)hipFree(rows);
+      fprintf(stderr, "[piece stats] rank %d: local in-degree bin, rows, edges, pieces, pieces/edge; "
+              "by segment kind LDS / L2-hot / cold: edges, pieces\n", rank);
+      for (int b = 0; b < PS_BINS; ++b) {
+        if (!hr[b]) continue;
+        unsigned long long e = 0, pc = 0;
+        for (int k = 0; k < 3; ++k) { pc += hh[b * 6 + k * 2]; e += hh[b * 6 + k * 2 + 1]; }
+        fprintf(stderr, "[piece stats] deg [%u, %u) rows %llu edges %llu pieces %llu p/e %.3f | "
+                "LDS %llu %llu | hot %llu %llu | cold %llu %llu\n",
+                1u << b, b >= 31 ? 0xFFFFFFFFu : (2u << b), hr[b], e, pc, e ? double(pc) / e : 0.0,
+                hh[b * 6 + 1], hh[b * 6 + 0], hh[b * 6 + 3], hh[b * 6 + 2], hh[b * 6 + 5], hh[b * 6 + 4]);
+      }
+    }
     // fill the empty runs: T[NB][k] = end of stream k, T[b][k] = T[b+1][k] where empty
     std::vector<uint32_t> hT(tn), hs(RBk.NS);
     HIPTRY(hipMemcpyAsync(hT.data(), g->runs, 4 * tn, hipMemcpyDeviceToHost, s));
