@@ -498,7 +498,7 @@ __device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[
 // NT: 2 = non-temporal piece stores.  SPLIT: dedicated L2 waves (A.l2w).  STAMPS: PR_STAMPS
 // diagnostics.  The variants are separate instantiations so that the default one carries no
 // register cost for the others.
-template <int NT, bool SPLIT, bool STAMPS>
+template <int NT, bool SPLIT, bool STAMPS, bool NTC = false>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
   const uint32_t j = blockIdx.x % NSLICE;
@@ -560,8 +560,13 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // groups are padded to whole tasks: these loads never leave the stream buffers
     if (lds_task) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
-      cn[0] = cp[0];
-      cn[1] = cp[1];
+      if constexpr (NTC) {  // PR_NTC experiment: non-temporal LDS-task column loads
+        cn[0] = __builtin_nontemporal_load(cp);
+        cn[1] = __builtin_nontemporal_load(cp + 1);
+      } else {
+        cn[0] = cp[0];
+        cn[1] = cp[1];
+      }
     } else {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
 #pragma unroll
@@ -2113,6 +2118,17 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
     attr_set = true;
   }
   const bool split = A.l2w && A.nlds, st = A.stamps != nullptr;
+  static const bool ntc = env_int("PR_NTC", 0) != 0;
+  static bool nattr = false;
+  if (!nattr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_stream<2, true, false, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    nattr = true;
+  }
+  if (ntc && split && !st && g->tune.nt == 2) {
+    hipLaunchKernelGGL((spmv_stream<2, true, false, true>), gr, bl, lds, s, A);
+    return;
+  }
   if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
   else if (split && st) hipLaunchKernelGGL((spmv_stream<2, true, true>), gr, bl, lds, s, A);
   else if (split) hipLaunchKernelGGL((spmv_stream<2, true, false>), gr, bl, lds, s, A);
