@@ -560,7 +560,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // groups are padded to whole tasks: these loads never leave the stream buffers
     if (lds_task) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
-      if constexpr (NTC) {  // PR_NTC experiment: non-temporal LDS-task column loads
+      if constexpr (NTC) {  // PR_NTC experiment: non-temporal stream-word loads
         cn[0] = __builtin_nontemporal_load(cp);
         cn[1] = __builtin_nontemporal_load(cp + 1);
       } else {
@@ -570,10 +570,14 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     } else {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) cn[q] = cp[q];
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (NTC) cn[q] = __builtin_nontemporal_load(cp + q);
+        else cn[q] = cp[q];
+      }
     }
     const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
-    bnx = bits[so / EPL];
+    if constexpr (NTC) bnx = __builtin_nontemporal_load(bits + so / EPL);
+    else bnx = bits[so / EPL];
     tpn = tpa[tt];
   };
   // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
