@@ -498,7 +498,7 @@ __device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[
 // NT: 2 = non-temporal piece stores.  SPLIT: dedicated L2 waves (A.l2w).  STAMPS: PR_STAMPS
 // diagnostics.  The variants are separate instantiations so that the default one carries no
 // register cost for the others.
-template <int NT, bool SPLIT, bool STAMPS, bool NTC = false>
+template <int NT, bool SPLIT, bool STAMPS, int NTC = 0>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
   const uint32_t j = blockIdx.x % NSLICE;
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // groups are padded to whole tasks: these loads never leave the stream buffers
     if (lds_task) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
-      if constexpr (NTC) {  // PR_NTC experiment: non-temporal stream-word loads
+      if constexpr ((NTC & 1) != 0) {  // PR_NTC bits: non-temporal loads of 1 col16, 2 col, 4 flags
         cn[0] = __builtin_nontemporal_load(cp);
         cn[1] = __builtin_nontemporal_load(cp + 1);
       } else {
@@ -571,12 +571,12 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col + o);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if constexpr (NTC) cn[q] = __builtin_nontemporal_load(cp + q);
+        if constexpr ((NTC & 2) != 0) cn[q] = __builtin_nontemporal_load(cp + q);
         else cn[q] = cp[q];
       }
     }
     const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
-    if constexpr (NTC) bnx = __builtin_nontemporal_load(bits + so / EPL);
+    if constexpr ((NTC & 4) != 0) bnx = __builtin_nontemporal_load(bits + so / EPL);
     else bnx = bits[so / EPL];
     tpn = tpa[tt];
   };
@@ -2122,15 +2122,19 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
     attr_set = true;
   }
   const bool split = A.l2w && A.nlds, st = A.stamps != nullptr;
-  static const bool ntc = env_int("PR_NTC", 0) != 0;
+  static const int ntc = env_int("PR_NTC", 0);
   static bool nattr = false;
   if (!nattr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&spmv_stream<2, true, false, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 1>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, false, 3>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, false, 5>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     nattr = true;
   }
   if (ntc && split && !st && g->tune.nt == 2) {
-    hipLaunchKernelGGL((spmv_stream<2, true, false, true>), gr, bl, lds, s, A);
+    if (ntc == 1) hipLaunchKernelGGL((spmv_stream<2, true, false, 1>), gr, bl, lds, s, A);
+    else if (ntc == 3) hipLaunchKernelGGL((spmv_stream<2, true, false, 3>), gr, bl, lds, s, A);
+    else hipLaunchKernelGGL((spmv_stream<2, true, false, 5>), gr, bl, lds, s, A);
     return;
   }
   if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
