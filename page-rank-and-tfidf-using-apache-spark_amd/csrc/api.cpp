@@ -137,7 +137,7 @@ int build_device(pr_ctx* c, const prmi::BuildInput& in0) {
             U(4ull * (g.ntask + 1ull)), U(std::min<uint64_t>(xlds, 8ull * g.X)),
             U(8ull * g.X - std::min<uint64_t>(xlds, 8ull * g.X)), U(8ull * g.n_pieces),
             U(8ull * g.n_pieces), U(2ull * g.n_pieces),
-            U(10ull * g.n_lines + 4ull * g.n_runs + 12ull * g.nb_rows), U(4ull * g.lrows),
+            U(12ull * g.n_lines + 4ull * g.n_runs + 12ull * g.nb_rows), U(4ull * g.lrows),
             U(8ull * g.lA), U(g.n_col16), U(g.n_col32), U(g.n_lines), U(g.n_runs));
   }
   return PR_OK;

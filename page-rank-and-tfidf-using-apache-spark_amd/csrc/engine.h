@@ -140,7 +140,7 @@ struct DevGraph {
   uint32_t* ne_off = nullptr;     // [nb_rows + 1]
   uint32_t* l_off = nullptr;      // [nb_rows + 1] first line of each block
   uint32_t* btot = nullptr;       // [nb_rows] pieces per block
-  uint16_t* lfirst = nullptr;     // [lines] block-relative run of the line's first piece
+  uint32_t* lfirst = nullptr;     // [lines] block-relative run of the line's first piece
   uint64_t* lmask = nullptr;      // [lines] run starts inside the line
   uint32_t* meta = nullptr;
   uint32_t* perm = nullptr;       // internal -> original

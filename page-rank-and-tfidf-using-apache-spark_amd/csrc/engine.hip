@@ -178,8 +178,8 @@ struct RowArgs {
   const uint32_t* ne_off;  // [NB + 1] first run of each block in nebase
   const uint32_t* l_off;   // [NB + 1] first line of each block in lfirst / lmask
   const uint32_t* tot;     // [NB] pieces of each block
-  const uint16_t* lfirst;  // [lines] run (block-relative) of each line's first piece
-  const uint64_t* lmask;   // [lines] bit j: piece j of the line starts a run (j >= 1)
+  const uint32_t* lfirst;  // [lines + pad] run (block-relative) of each line's first piece
+  const uint64_t* lmask;   // [lines + pad] bit j: piece j of the line starts a run (j >= 1)
   const double* partial;   // per-piece partial sums of this round
   const uint16_t* roff;    // per-piece row offset inside its block
   uint32_t NS, nbA, lA, lrows;
@@ -303,13 +303,20 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   uint32_t ra[EPR], rbuf[EPR];
   uint32_t fa[EPR];
   uint64_t ma[EPR];
-  // line maps of a step (wave-uniform loads), fetched one step ahead of their use
+  // line maps of a step, fetched one step ahead of their use: wave-uniform, so scalar loads
+  // (constant address space + a readfirstlane index) that leave the vector memory pipe to
+  // the piece reads; the arrays are padded by 2 * EPR lines, so a step may read past the
+  // block's lines (those lanes are masked)
+  typedef const __attribute__((address_space(4))) uint32_t* cu32p;
+  typedef const __attribute__((address_space(4))) uint64_t* cu64p;
+  const cu32p lf = (cu32p)(A.lfirst);
+  const cu64p lm = (cu64p)(A.lmask);
   auto maps = [&](uint32_t L) {
+    const uint32_t Lb = __builtin_amdgcn_readfirstlane(L0 + L);
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
-      const uint32_t Lu = min(L + u, nl ? nl - 1 : 0u);
-      fa[u] = A.lfirst[L0 + Lu];
-      ma[u] = A.lmask[L0 + Lu];
+      fa[u] = lf[Lb + u];
+      ma[u] = lm[Lb + u];
     }
   };
   auto issue = [&](uint32_t L, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
@@ -1998,7 +2005,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     {
       const uint32_t NB = RBk.NB;
       std::vector<uint32_t> hne, hneoff(NB + 1), hloff(NB + 1), htot(NB);
-      std::vector<uint16_t> hlf;
+      std::vector<uint32_t> hlf;
       std::vector<uint64_t> hlm;
       std::vector<uint32_t> pre_q;  // per block: pre of each non-empty run
       uint64_t lines = 0;
@@ -2023,7 +2030,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
           while (q + 1 < pre_q.size() && pre_q[q + 1] <= i0) ++q;
           uint64_t m = 0;
           for (uint32_t r = q + 1; r < pre_q.size() && pre_q[r] < i0 + 64; ++r) m |= 1ull << (pre_q[r] - i0);
-          hlf.push_back(static_cast<uint16_t>(q));
+          hlf.push_back(static_cast<uint32_t>(q));
           hlm.push_back(m);
         }
         lines += nl;
@@ -2040,14 +2047,16 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
       TRY(dmalloc(&g->ne_off, NB + 1ull, err));
       TRY(dmalloc(&g->l_off, NB + 1ull, err));
       TRY(dmalloc(&g->btot, NB, err));
-      TRY(dmalloc(&g->lfirst, lines, err));
-      TRY(dmalloc(&g->lmask, lines, err));
+      TRY(dmalloc(&g->lfirst, lines + 2 * EPR, err));  // + the row launch's read-ahead
+      TRY(dmalloc(&g->lmask, lines + 2 * EPR, err));
+      HIPTRY(hipMemsetAsync(g->lfirst, 0, 4ull * (lines + 2 * EPR), s));
+      HIPTRY(hipMemsetAsync(g->lmask, 0, 8ull * (lines + 2 * EPR), s));
       if (!hne.empty()) HIPTRY(hipMemcpyAsync(g->nebase, hne.data(), 4 * hne.size(), hipMemcpyHostToDevice, s));
       HIPTRY(hipMemcpyAsync(g->ne_off, hneoff.data(), 4ull * (NB + 1), hipMemcpyHostToDevice, s));
       HIPTRY(hipMemcpyAsync(g->l_off, hloff.data(), 4ull * (NB + 1), hipMemcpyHostToDevice, s));
       if (NB) HIPTRY(hipMemcpyAsync(g->btot, htot.data(), 4ull * NB, hipMemcpyHostToDevice, s));
       if (lines) {
-        HIPTRY(hipMemcpyAsync(g->lfirst, hlf.data(), 2 * lines, hipMemcpyHostToDevice, s));
+        HIPTRY(hipMemcpyAsync(g->lfirst, hlf.data(), 4 * lines, hipMemcpyHostToDevice, s));
         HIPTRY(hipMemcpyAsync(g->lmask, hlm.data(), 8 * lines, hipMemcpyHostToDevice, s));
       }
       HIPTRY(hipStreamSynchronize(s));
