@@ -126,6 +126,7 @@ struct DevGraph {
   uint32_t nseg = 0;              // segments per slice (LDS blocks + L2-hot + cold)
   uint64_t n_pieces = 0, n_pairs = 0;
   uint64_t n_lines = 0, n_runs = 0;  // row-launch 64-piece lines, non-empty (block, stream) runs
+  uint64_t n_groups = 0;             // row-launch 8-line groups
   uint64_t stream_len = 0;        // padded length of col (multiple of TASK)
   // device arrays
   uint32_t* col = nullptr;        // [n_col32] L2-group edges: x position of the source
@@ -142,6 +143,8 @@ struct DevGraph {
   uint32_t* btot = nullptr;       // [nb_rows] pieces per block
   uint32_t* lfirst = nullptr;     // [lines] block-relative run of the line's first piece
   uint64_t* lmask = nullptr;      // [lines] run starts inside the line
+  uint32_t* goff = nullptr;       // [nb_rows + 1] first 8-line group of each block
+  uint16_t* roffL = nullptr;      // [groups * 64 * 8] row offsets in row-launch order
   uint32_t* meta = nullptr;
   uint32_t* perm = nullptr;       // internal -> original
   uint32_t* outdeg = nullptr;     // by original id

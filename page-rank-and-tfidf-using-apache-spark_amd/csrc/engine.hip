@@ -181,7 +181,9 @@ struct RowArgs {
   const uint32_t* lfirst;  // [lines + pad] run (block-relative) of each line's first piece
   const uint64_t* lmask;   // [lines + pad] bit j: piece j of the line starts a run (j >= 1)
   const double* partial;   // per-piece partial sums of this round
-  const uint16_t* roff;    // per-piece row offset inside its block
+  const uint16_t* roffL;   // row offsets in row-launch order: per 8-line group, lane-major
+                           // (lane l's 8 values in one 16-byte word)
+  const uint32_t* goff;    // [NB + 1] first 8-line group of each block
   uint32_t NS, nbA, lA, lrows;
   uint32_t rb;             // rows per block (<= RB)
   uint32_t nbH, rbH, lH;   // heavy blocks: the first lH class-A rows in nbH blocks of rbH rows
@@ -293,10 +295,13 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   for (uint32_t q = tid; q < nne; q += BLOCK) nb[q] = A.nebase[ne0 + q];
   const uint32_t tot = A.tot[b];
   const uint32_t L0 = A.l_off[b], nl = A.l_off[b + 1] - L0;
+  const uint32_t G0 = A.goff[b];
   __syncthreads();
-  // this wave's quarter of the lines; a step = EPR lines, lane l takes piece l of each
-  const uint32_t lo = static_cast<uint32_t>(static_cast<uint64_t>(nl) * wv / 4);
-  const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(nl) * (wv + 1) / 4);
+  // this wave's quarter of the block's 8-line groups; a step = one group (EPR lines), lane l
+  // takes piece l of each line and the group's 8 row offsets of lane l in one 16-byte load
+  const uint32_t ng = (nl + EPR - 1) / EPR;
+  const uint32_t lo = (ng * wv / 4) * EPR;
+  const uint32_t hi = min((ng * (wv + 1) / 4) * EPR, nl);
   double* aw = acc[wv];
   const uint64_t lbits = (2ull << lane) - 2ull;  // bits 1 .. lane
   double va[EPR], vb[EPR], sink = 0.0;
@@ -319,6 +324,7 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
       ma[u] = lm[Lb + u];
     }
   };
+  typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
   auto issue = [&](uint32_t L, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
@@ -326,8 +332,11 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
       const uint32_t q = fa[u] + static_cast<uint32_t>(__popcll(ma[u] & lbits));
       const uint32_t pc = (L + u < hi && i < tot) ? nb[q] + i : 0u;  // never past the pieces
       vv[u] = A.partial[pc];
-      rr[u] = A.roff[pc];
     }
+    const u16x8 r8 = *reinterpret_cast<const u16x8*>(
+        A.roffL + ((static_cast<uint64_t>(G0 + L / EPR) * 64u) + static_cast<uint32_t>(lane)) * EPR);
+#pragma unroll
+    for (int u = 0; u < EPR; ++u) rr[u] = r8[u];
     maps(L + EPR);
   };
   auto add = [&](uint32_t L, const double (&vv)[EPR], const uint32_t (&rr)[EPR]) {
@@ -1242,6 +1251,32 @@ __global__ void k_piece_rows(const uint64_t* key, uint64_t n, StreamGeo G, uint3
   }
 }
 
+// row offsets in row-launch order (RowArgs::roffL): one workgroup per block; each wave walks
+// the block's lines exactly as spmv_rows does and stores lane l's offsets of an 8-line group
+// contiguously
+__global__ __launch_bounds__(BLOCK) void k_roff_lines(const uint16_t* roff, const uint32_t* nebase,
+                                                      const uint32_t* ne_off, const uint32_t* l_off,
+                                                      const uint32_t* btot, const uint32_t* lfirst,
+                                                      const uint64_t* lmask, const uint32_t* goff,
+                                                      uint16_t* roffL) {
+  const uint32_t b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t L0 = l_off[b], nl = l_off[b + 1] - L0, tot = btot[b], ne0 = ne_off[b];
+  const uint32_t G0 = goff[b], ng = (nl + EPR - 1) / EPR;
+  const uint64_t lbits = (2ull << lane) - 2ull;
+  for (uint32_t gi = wv; gi < ng; gi += BLOCK / 64) {
+    for (int u = 0; u < EPR; ++u) {
+      const uint32_t L = gi * EPR + u, i = L * 64u + static_cast<uint32_t>(lane);
+      uint16_t r = 0;
+      if (L < nl && i < tot) {
+        const uint32_t q = lfirst[L0 + L] + static_cast<uint32_t>(__popcll(lmask[L0 + L] & lbits));
+        r = roff[nebase[ne0 + q] + i];
+      }
+      roffL[((static_cast<uint64_t>(G0 + gi) * 64u) + static_cast<uint32_t>(lane)) * EPR + u] = r;
+    }
+  }
+}
+
 // PR_PIECE_STATS (build-time report): pieces and edges by row in-degree bin (bin b holds
 // in-degrees [2^b, 2^(b+1))) and by segment kind (0 LDS block, 1 L2-hot, 2 cold)
 constexpr int PS_BINS = 24;
@@ -1514,6 +1549,7 @@ void dev_free(DevGraph* g) {
   auto F = [](void* p) { if (p) (void)hipFree(p); };
   F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->roff); F(g->runs);
   F(g->nebase); F(g->ne_off); F(g->l_off); F(g->btot); F(g->lfirst); F(g->lmask);
+  F(g->goff); F(g->roffL);
   F(g->d_gtask); F(g->d_gstart); F(g->d_gbase); F(g->col16);
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
@@ -2059,6 +2095,20 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
         HIPTRY(hipMemcpyAsync(g->lfirst, hlf.data(), 4 * lines, hipMemcpyHostToDevice, s));
         HIPTRY(hipMemcpyAsync(g->lmask, hlm.data(), 8 * lines, hipMemcpyHostToDevice, s));
       }
+      // 8-line groups per block and the row offsets in row-launch order
+      std::vector<uint32_t> hgoff(NB + 1);
+      uint64_t groups = 0;
+      for (uint32_t bb = 0; bb < NB; ++bb) {
+        hgoff[bb] = static_cast<uint32_t>(groups);
+        groups += (hloff[bb + 1] - hloff[bb] + EPR - 1) / EPR;
+      }
+      hgoff[NB] = static_cast<uint32_t>(groups);
+      g->n_groups = groups;
+      TRY(dmalloc(&g->goff, NB + 1ull, err));
+      TRY(dmalloc(&g->roffL, std::max<uint64_t>(groups, 1) * 64 * EPR, err));
+      HIPTRY(hipMemcpyAsync(g->goff, hgoff.data(), 4ull * (NB + 1), hipMemcpyHostToDevice, s));
+      if (NB) hipLaunchKernelGGL(k_roff_lines, dim3(NB), dim3(BLOCK), 0, s, g->roff, g->nebase, g->ne_off, g->l_off, g->btot, g->lfirst, g->lmask, g->goff, g->roffL);
+      HIPTRY(hipGetLastError());
       HIPTRY(hipStreamSynchronize(s));
     }
     HIPTRY(hipStreamSynchronize(s));
@@ -2238,7 +2288,8 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
   A.lfirst = g->lfirst;
   A.lmask = g->lmask;
   A.partial = g->partial;
-  A.roff = g->roff;
+  A.roffL = g->roffL;
+  A.goff = g->goff;
   A.dbg = static_cast<uint32_t>(g->tune.dbg);
   A.NS = g->n_streams;
   A.rb = g->row_rb;
