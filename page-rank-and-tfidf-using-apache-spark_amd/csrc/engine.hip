@@ -194,7 +194,8 @@ struct RowArgs {
   const IterState* st;
   uint64_t* shards;
   uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
-  uint32_t dbg;              // PR_DBG timing experiments: 16 no LDS adds, 32 no epilogue, 64 no pieces
+  uint32_t dbg;              // PR_DBG timing experiments: 16 no LDS adds, 32 no epilogue, 64 no
+                             // pieces; 128 non-temporal piece loads (not timing-only)
   double base, r0;           // damping base (0.15) and initial rank (1.0), or their /N_tot forms
   uint32_t b0;               // first row block of this launch (the row launch may be chunked)
   uint32_t xg, xfull;        // XCD groups: xg consecutive blocks per XCD in the first xfull
@@ -331,7 +332,8 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
       const uint32_t i = (L + u) * 64u + static_cast<uint32_t>(lane);
       const uint32_t q = fa[u] + static_cast<uint32_t>(__popcll(ma[u] & lbits));
       const uint32_t pc = (L + u < hi && i < tot) ? nb[q] + i : 0u;  // never past the pieces
-      vv[u] = A.partial[pc];
+      if (A.dbg & 128u) vv[u] = __builtin_nontemporal_load(A.partial + pc);  // experiment
+      else vv[u] = A.partial[pc];
     }
     const u16x8 r8 = *reinterpret_cast<const u16x8*>(
         A.roffL + ((static_cast<uint64_t>(G0 + L / EPR) * 64u) + static_cast<uint32_t>(lane)) * EPR);
