@@ -199,7 +199,6 @@ struct RowArgs {
   double base, r0;           // damping base (0.15) and initial rank (1.0), or their /N_tot forms
   uint32_t b0;               // first row block of this launch (the row launch may be chunked)
   uint32_t xg, xfull;        // XCD groups: xg consecutive blocks per XCD in the first xfull
-  uint32_t nbl;              // blocks of this launch (the persistent form loops over them)
 };
 
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
@@ -380,152 +379,6 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   if (clsB || MODE == 2) {  // uniform over the workgroup
     __syncthreads();
     flush_records(A, lds);
-  }
-}
-
-// The persistent form of the row launch: a workgroup takes blocks k = blockIdx, blockIdx +
-// gridDim, ... and loads the next block's header (run bases, row metadata) while the current
-// block's pieces stream in, so the per-block latency chain (offsets -> run bases -> first
-// piece) is paid once per workgroup instead of once per block.  Same arithmetic, same order.
-template <int MODE>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void spmv_rows_p(RowArgs A) {
-  __shared__ double acc[4][RB];
-  __shared__ uint32_t nb[MAX_NS];   // the block's non-empty runs: start - pre
-  __shared__ uint64_t lds[4][REC_WORDS];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < 4 * RB; i += BLOCK) (&acc[0][0])[i] = 0.0;
-  for (int i = tid; i < 4 * REC_WORDS; i += BLOCK) (&lds[0][0])[i] = 0;
-  constexpr int RPT = RB / BLOCK;   // rows per thread
-  auto block_of = [&](uint32_t k) -> uint32_t {
-    // XCD groups: k and blockIdx agree mod 8 (gridDim is a multiple of 8), so each XCD keeps
-    // runs of xg consecutive blocks
-    if (k < A.xfull) {
-      const uint32_t span = NSLICE * A.xg, r = k % span;
-      k = (k - r) + (r % NSLICE) * A.xg + r / NSLICE;
-    }
-    return k + A.b0;
-  };
-  // ---- the next block's header, held in registers until it starts: its offsets and its
-  // rows' metadata (the run bases follow at the block start, beside its first line maps)
-  uint32_t hb, hne0, hnne, hL0, hnl, htot, hG0;
-  uint32_t hmt[RPT];
-  double hro[RPT];
-  auto load_hdr = [&](uint32_t b) {
-    hb = b;
-    const bool clsB = b >= A.nbA, heavy = b < A.nbH;
-    const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * A.rb : (heavy ? b * A.rbH : A.lH + (b - A.nbH) * A.rb);
-    const uint32_t rb1 = min(rb0 + (heavy ? A.rbH : A.rb), clsB ? A.lrows : A.lA);
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      const uint32_t row = rb0 + tid + q * BLOCK;
-      hmt[q] = row < rb1 ? A.meta[row] : 0u;
-      hro[q] = 0.0;
-      if (MODE == 2 && row < rb1) hro[q] = A.r_old ? A.r_old[row] : A.r0;
-    }
-    hne0 = A.ne_off[b];
-    hnne = A.ne_off[b + 1] - hne0;
-    hL0 = A.l_off[b];
-    hnl = A.l_off[b + 1] - hL0;
-    htot = A.tot[b];
-    hG0 = A.goff[b];
-  };
-  uint32_t k = blockIdx.x;
-  if (k >= A.nbl) return;
-  load_hdr(block_of(k));
-  const uint64_t lbits = (2ull << lane) - 2ull;  // bits 1 .. lane
-  typedef const __attribute__((address_space(4))) uint32_t* cu32p;
-  typedef const __attribute__((address_space(4))) uint64_t* cu64p;
-  const cu32p lf = (cu32p)(A.lfirst);
-  const cu64p lm = (cu64p)(A.lmask);
-  typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
-  double* aw = acc[wv];
-  uint64_t* lw = lds[wv];
-  for (;;) {
-    // ---- start block b: run bases to LDS (their loads beside the first line maps)
-    const uint32_t b = hb, tot = htot, L0 = hL0, nl = hnl, G0 = hG0;
-    for (uint32_t q = tid; q < hnne; q += BLOCK) nb[q] = A.nebase[hne0 + q];
-    uint32_t mt[RPT];
-    double ro[RPT];
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      mt[q] = hmt[q];
-      ro[q] = hro[q];
-    }
-    const bool clsB = b >= A.nbA, heavy = b < A.nbH;
-    const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * A.rb : (heavy ? b * A.rbH : A.lH + (b - A.nbH) * A.rb);
-    const uint32_t rb1 = min(rb0 + (heavy ? A.rbH : A.rb), clsB ? A.lrows : A.lA);
-    const uint32_t ng = (nl + EPR - 1) / EPR;
-    const uint32_t lo = (ng * wv / 4) * EPR;
-    const uint32_t hi = min((ng * (wv + 1) / 4) * EPR, nl);
-    double va[EPR], vb[EPR], sink = 0.0;
-    uint32_t ra[EPR], rbuf[EPR];
-    uint32_t fa[EPR];
-    uint64_t ma[EPR];
-    auto maps = [&](uint32_t L) {
-      const uint32_t Lb = __builtin_amdgcn_readfirstlane(L0 + L);
-#pragma unroll
-      for (int u = 0; u < EPR; ++u) {
-        fa[u] = lf[Lb + u];
-        ma[u] = lm[Lb + u];
-      }
-    };
-    auto issue = [&](uint32_t L, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
-#pragma unroll
-      for (int u = 0; u < EPR; ++u) {
-        const uint32_t i = (L + u) * 64u + static_cast<uint32_t>(lane);
-        const uint32_t q = fa[u] + static_cast<uint32_t>(__popcll(ma[u] & lbits));
-        const uint32_t pc = (L + u < hi && i < tot) ? nb[q] + i : 0u;  // never past the pieces
-        vv[u] = A.partial[pc];
-      }
-      const u16x8 r8 = *reinterpret_cast<const u16x8*>(
-          A.roffL + ((static_cast<uint64_t>(G0 + L / EPR) * 64u) + static_cast<uint32_t>(lane)) * EPR);
-#pragma unroll
-      for (int u = 0; u < EPR; ++u) rr[u] = r8[u];
-      maps(L + EPR);
-    };
-    auto add = [&](uint32_t L, const double (&vv)[EPR], const uint32_t (&rr)[EPR]) {
-#pragma unroll
-      for (int u = 0; u < EPR; ++u)
-        if (L + u < hi && (L + u) * 64u + static_cast<uint32_t>(lane) < tot) {
-          if (A.dbg & 16u) sink += vv[u] + rr[u];
-          else atomicAdd(&aw[rr[u]], vv[u]);
-        }
-    };
-    const uint32_t hi_loop = (A.dbg & 64u) ? lo : hi;
-    if (lo < hi_loop) maps(lo);
-    __syncthreads();  // nb written; acc and the records cleared by the previous block
-    if (lo < hi_loop) issue(lo, va, ra);
-    // the next block's header, in flight beside this block's pieces
-    const uint32_t kn = k + gridDim.x;
-    const bool more = kn < A.nbl;
-    if (more) load_hdr(block_of(kn));
-    for (uint32_t L = lo; L < hi_loop; L += 2 * EPR) {
-      const bool n1 = L + EPR < hi, n2 = L + 2 * EPR < hi;
-      if (n1) issue(L + EPR, vb, rbuf);
-      add(L, va, ra);
-      if (n2) issue(L + 2 * EPR, va, ra);
-      if (n1) add(L + EPR, vb, rbuf);
-    }
-    if (A.dbg & 16u) aw[lane] = sink;
-    __syncthreads();
-    // ---- epilogue over the block's rows; each thread clears the accumulators it read
-    const double a = A.st->a;
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      const int l = tid + q * BLOCK;
-      const uint32_t row = rb0 + l;
-      double c = (acc[0][l] + acc[1][l]) + (acc[2][l] + acc[3][l]);
-      acc[0][l] = acc[1][l] = acc[2][l] = acc[3][l] = 0.0;
-      if (A.dbg & 64u) c = 1.0;
-      row_finish<MODE>(A, a, clsB ? 1u : 0u, row, c, row < rb1, mt[q], ro[q], lw);
-    }
-    if (clsB || MODE == 2) {  // uniform over the workgroup
-      __syncthreads();
-      flush_records(A, lds);
-      if (tid < REC_WORDS) lds[0][tid] = lds[1][tid] = lds[2][tid] = lds[3][tid] = 0;
-    }
-    if (!more) break;
-    k = kn;
   }
 }
 
@@ -2463,22 +2316,7 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
   A.b0 = b0;
   A.xg = std::max(1u, g->tune.rxg);
   A.xfull = (b1 - b0) / (NSLICE * A.xg) * (NSLICE * A.xg);
-  A.nbl = b1 - b0;
-  static const int persist = env_int("PR_RPERSIST", 1);
-  if (b1 > b0 && persist && mode != 2) {  // (tracked rounds keep the per-block form: registers)
-    // 4 workgroups per CU (LDS-bound), a multiple of 8 so each keeps its XCD
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    }
-    uint32_t grid = std::min<uint32_t>(A.nbl, 4u * static_cast<uint32_t>(ncu) * std::max(1, persist));
-    if (grid >= 8) grid &= ~7u;
-    const dim3 gr(grid), bl(BLOCK);
-    if (mode == 0) hipLaunchKernelGGL((spmv_rows_p<0>), gr, bl, 0, s, A);
-    else hipLaunchKernelGGL((spmv_rows_p<1>), gr, bl, 0, s, A);
-  } else if (b1 > b0) {
+  if (b1 > b0) {
     const dim3 gr(b1 - b0), bl(BLOCK);
     if (mode == 0) hipLaunchKernelGGL((spmv_rows<0>), gr, bl, 0, s, A);
     else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1>), gr, bl, 0, s, A);
