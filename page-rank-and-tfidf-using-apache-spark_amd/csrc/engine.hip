@@ -293,11 +293,9 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
     if (MODE == 2 && row < rb1) ro[q] = A.r_old ? A.r_old[row] : A.r0;
   }
   const uint32_t ne0 = A.ne_off[b], nne = A.ne_off[b + 1] - ne0;
-  for (uint32_t q = tid; q < nne; q += BLOCK) nb[q] = A.nebase[ne0 + q];
   const uint32_t tot = A.tot[b];
   const uint32_t L0 = A.l_off[b], nl = A.l_off[b + 1] - L0;
   const uint32_t G0 = A.goff[b];
-  __syncthreads();
   // this wave's quarter of the block's 8-line groups; a step = one group (EPR lines), lane l
   // takes piece l of each line and the group's 8 row offsets of lane l in one 16-byte load
   const uint32_t ng = (nl + EPR - 1) / EPR;
@@ -351,10 +349,10 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
       }
   };
   const uint32_t hi_loop = (A.dbg & 64u) ? lo : hi;  // timing: no piece loads at all
-  if (lo < hi_loop) {
-    maps(lo);
-    issue(lo, va, ra);
-  }
+  if (lo < hi_loop) maps(lo);  // (scalar loads: in flight beside the run bases)
+  for (uint32_t q = tid; q < nne; q += BLOCK) nb[q] = A.nebase[ne0 + q];
+  __syncthreads();
+  if (lo < hi_loop) issue(lo, va, ra);
   for (uint32_t L = lo; L < hi_loop; L += 2 * EPR) {
     const bool n1 = L + EPR < hi, n2 = L + 2 * EPR < hi;
     if (n1) issue(L + EPR, vb, rbuf);
