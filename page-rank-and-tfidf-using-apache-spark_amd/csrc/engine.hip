@@ -468,37 +468,45 @@ __device__ __forceinline__ double wave_seg_scan(double S, int F, int lane) {
   return S;
 }
 
-// Sixteen buffer gathers x[off/8] into v[k], then one s_waitcnt: the asm block ends with its
-// loads landed, so the compiler never sees an in-flight destination.  Padding lanes carry an
-// offset past the buffer's range and read 0 (no EXEC masks needed).
+// Sixteen exec-masked buffer gathers x[off/8] into v[k] (lanes outside gm[k] keep v[k]),
+// then one s_waitcnt: the asm block ends with its loads landed, so the compiler never sees
+// an in-flight destination.
 __device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[EPL],
-                                         __amdgpu_buffer_rsrc_t xr) {
+                                         const uint64_t (&gm)[EPL], __amdgpu_buffer_rsrc_t xr) {
+  uint64_t sv;
   asm volatile(
-      "buffer_load_dwordx2 %[d0], %[o0], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d1], %[o1], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d2], %[o2], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d3], %[o3], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d4], %[o4], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d5], %[o5], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d6], %[o6], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d7], %[o7], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d8], %[o8], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d9], %[o9], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d10], %[o10], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d11], %[o11], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d12], %[o12], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d13], %[o13], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d14], %[o14], %[rs], 0 offen\n"
-      "buffer_load_dwordx2 %[d15], %[o15], %[rs], 0 offen\n"
+      "s_mov_b64 %[sv], exec\n"
+      "s_and_b64 exec, %[sv], %[m0]\n  buffer_load_dwordx2 %[d0], %[o0], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m1]\n  buffer_load_dwordx2 %[d1], %[o1], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m2]\n  buffer_load_dwordx2 %[d2], %[o2], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m3]\n  buffer_load_dwordx2 %[d3], %[o3], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m4]\n  buffer_load_dwordx2 %[d4], %[o4], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m5]\n  buffer_load_dwordx2 %[d5], %[o5], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m6]\n  buffer_load_dwordx2 %[d6], %[o6], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m7]\n  buffer_load_dwordx2 %[d7], %[o7], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m8]\n  buffer_load_dwordx2 %[d8], %[o8], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m9]\n  buffer_load_dwordx2 %[d9], %[o9], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m10]\n buffer_load_dwordx2 %[d10], %[o10], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m11]\n buffer_load_dwordx2 %[d11], %[o11], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m12]\n buffer_load_dwordx2 %[d12], %[o12], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m13]\n buffer_load_dwordx2 %[d13], %[o13], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m14]\n buffer_load_dwordx2 %[d14], %[o14], %[rs], 0 offen\n"
+      "s_and_b64 exec, %[sv], %[m15]\n buffer_load_dwordx2 %[d15], %[o15], %[rs], 0 offen\n"
+      "s_mov_b64 exec, %[sv]\n"
       "s_waitcnt vmcnt(0)\n"
-      : [d0] "=&v"(v[0]), [d1] "=&v"(v[1]), [d2] "=&v"(v[2]), [d3] "=&v"(v[3]),
-        [d4] "=&v"(v[4]), [d5] "=&v"(v[5]), [d6] "=&v"(v[6]), [d7] "=&v"(v[7]),
-        [d8] "=&v"(v[8]), [d9] "=&v"(v[9]), [d10] "=&v"(v[10]), [d11] "=&v"(v[11]),
-        [d12] "=&v"(v[12]), [d13] "=&v"(v[13]), [d14] "=&v"(v[14]), [d15] "=&v"(v[15])
+      : [d0] "+v"(v[0]), [d1] "+v"(v[1]), [d2] "+v"(v[2]), [d3] "+v"(v[3]),
+        [d4] "+v"(v[4]), [d5] "+v"(v[5]), [d6] "+v"(v[6]), [d7] "+v"(v[7]),
+        [d8] "+v"(v[8]), [d9] "+v"(v[9]), [d10] "+v"(v[10]), [d11] "+v"(v[11]),
+        [d12] "+v"(v[12]), [d13] "+v"(v[13]), [d14] "+v"(v[14]), [d15] "+v"(v[15]),
+        [sv] "=&s"(sv)
       : [o0] "v"(qo[0]), [o1] "v"(qo[1]), [o2] "v"(qo[2]), [o3] "v"(qo[3]),
         [o4] "v"(qo[4]), [o5] "v"(qo[5]), [o6] "v"(qo[6]), [o7] "v"(qo[7]),
         [o8] "v"(qo[8]), [o9] "v"(qo[9]), [o10] "v"(qo[10]), [o11] "v"(qo[11]),
         [o12] "v"(qo[12]), [o13] "v"(qo[13]), [o14] "v"(qo[14]), [o15] "v"(qo[15]),
+        [m0] "s"(gm[0]), [m1] "s"(gm[1]), [m2] "s"(gm[2]), [m3] "s"(gm[3]),
+        [m4] "s"(gm[4]), [m5] "s"(gm[5]), [m6] "s"(gm[6]), [m7] "s"(gm[7]),
+        [m8] "s"(gm[8]), [m9] "s"(gm[9]), [m10] "s"(gm[10]), [m11] "s"(gm[11]),
+        [m12] "s"(gm[12]), [m13] "s"(gm[13]), [m14] "s"(gm[14]), [m15] "s"(gm[15]),
         [rs] "s"(xr)
       : "memory");
 }
@@ -551,9 +559,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   const uint32_t* __restrict__ col = A.col;
   const uint16_t* __restrict__ col16 = A.col16;
   const uint16_t* __restrict__ bits = A.bits;
-  // first piece of a task: wave-uniform, so a scalar load (constant address space)
-  const __attribute__((address_space(4))) uint32_t* tpa =
-      (const __attribute__((address_space(4))) uint32_t*)(A.task_piece);
+  const uint32_t* __restrict__ tpa = A.task_piece;
   double* __restrict__ part = A.partial;
   const uint32_t cm = A.colmask;
   const uint32_t ngs = A.nlds + 1;
@@ -588,7 +594,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
     if constexpr ((NTC & 4) != 0) bnx = __builtin_nontemporal_load(bits + so / EPL);
     else bnx = bits[so / EPL];
-    tpn = tpa[__builtin_amdgcn_readfirstlane(tt)];
+    tpn = tpa[tt];
   };
   // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
   // with 1/nlds of the L2 part's tasks (LDS-bound and L2-bound work side by side); with no
@@ -670,13 +676,18 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
         // sixteen buffer gathers issued back to back; PAD_COL lanes fall outside the buffer
         // range and read 0
         uint32_t qo[EPL];
+        uint64_t gm[EPL];
 #pragma unroll
-        for (int k = 0; k < EPL; ++k) qo[k] = (cv[k >> 2][k & 3] & cm) * 8u;
+        for (int k = 0; k < EPL; ++k) {
+          v[k] = 0.0;
+          qo[k] = (cv[k >> 2][k & 3] & cm) * 8u;
+          gm[k] = ~0ull;
+        }
         if (A.dbg & 2u) {
 #pragma unroll
           for (int k = 0; k < EPL; ++k) v[k] = static_cast<double>(qo[k] & 0xFFFF);
         } else {
-          gather16(v, qo, xr);
+          gather16(v, qo, gm, xr);
         }
       }
     // exclusive prefix (over lanes) of the piece starts -> first piece index of this lane
