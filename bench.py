@@ -2,8 +2,9 @@
 """Benchmark: PageRank rounds/s on R-MAT scale 26 (BASELINE.json config 4) on MI355X.
 
 A "step" is one PageRank round (PageRank.java:92-164): the fused pull SpMV over every
-distinct edge, dangling redistribution and damping, plus -- on more than one GPU -- the RCCL
-all-gather of the contribution vector.  The graph (R-MAT scale 26, edge factor 16, seed 4,
+distinct edge, dangling redistribution and damping, plus -- on more than one GPU -- the
+exchange of the contribution vector (grouped RCCL send/recv per row-launch chunk on a comm
+stream, and an all-gather of the exact per-rank record).  The graph (R-MAT scale 26, edge factor 16, seed 4,
 generated on the device; ~1.06e9 distinct edges) is resident in HBM before timing starts.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--no-cpu-baseline]
@@ -155,7 +156,8 @@ def main():
             "data": "synthetic (Graph500 R-MAT generated on device, Philox seed %d)" % a.seed,
             "config": {"workload": workload, "scale": a.scale, "edge_factor": a.edge_factor,
                        "vertices": n, "distinct_edges": nnz, "rounds_per_step": 1,
-                       "parallelism": f"rows dealt over {world} GPU(s), RCCL all-gather of x"
+                       "parallelism": f"rows dealt over {world} GPUs, chunked RCCL p2p "
+                                      f"exchange of x' overlapped with the row launch"
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
