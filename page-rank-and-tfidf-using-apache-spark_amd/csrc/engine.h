@@ -171,7 +171,6 @@ struct DevGraph {
   uint32_t nb_rows = 0, nb_rows_a = 0, n_streams = 0;
   uint32_t row_rb = 1024;          // rows per row-launch block
   uint32_t row_nbH = 0, row_rbH = 256, row_lH = 0;  // heavy row blocks (first lH rows)
-  uint32_t row_la = 0xFFFFFFFFu, row_lb = 0xFFFFFFFFu;  // first light block of class A / B
   Tuning tune;
 };
 

@@ -380,109 +380,6 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
   }
 }
 
-// Light row blocks (at most LIGHT_LINES lines and LIGHT_NS non-empty runs: the low in-degree
-// tails of class A and class B) are one wave's work: a workgroup takes 4 consecutive light
-// blocks, one per wave, with no workgroup barrier, so 16 light blocks per CU run their
-// latency chains (offsets -> run bases and line maps -> pieces) side by side.  One
-// accumulator per block: a fixed order (line order, lanes in order), deterministic.
-constexpr uint32_t LIGHT_LINES = 32;
-constexpr uint32_t LIGHT_NS = 256;
-template <int MODE>
-__global__ __launch_bounds__(BLOCK) void spmv_rows_light(RowArgs A, uint32_t bs, uint32_t be) {
-  __shared__ double acc[4][RB];
-  __shared__ uint32_t nbw[4][LIGHT_NS];
-  __shared__ uint64_t lds[4][REC_WORDS];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t b = bs + 4u * blockIdx.x + static_cast<uint32_t>(wv);
-  if (b >= be) return;  // wave-uniform; nothing below waits on other waves
-  double* aw = acc[wv];
-  uint32_t* nb = nbw[wv];
-  uint64_t* lw = lds[wv];
-  for (int i = lane; i < RB; i += 64) aw[i] = 0.0;
-  if (lane < REC_WORDS) lw[lane] = 0;
-  const bool clsB = b >= A.nbA, heavy = b < A.nbH;
-  const uint32_t rb0 = clsB ? A.lA + (b - A.nbA) * A.rb : (heavy ? b * A.rbH : A.lH + (b - A.nbH) * A.rb);
-  const uint32_t rb1 = min(rb0 + (heavy ? A.rbH : A.rb), clsB ? A.lrows : A.lA);
-  const uint32_t ne0 = A.ne_off[b], nne = A.ne_off[b + 1] - ne0;
-  const uint32_t tot = A.tot[b];
-  const uint32_t L0 = A.l_off[b], nl = A.l_off[b + 1] - L0;
-  const uint32_t G0 = A.goff[b];
-  typedef const __attribute__((address_space(4))) uint32_t* cu32p;
-  typedef const __attribute__((address_space(4))) uint64_t* cu64p;
-  const cu32p lf = (cu32p)(A.lfirst);
-  const cu64p lm = (cu64p)(A.lmask);
-  uint32_t fa[EPR];
-  uint64_t ma[EPR];
-  auto maps = [&](uint32_t L) {
-    const uint32_t Lb = __builtin_amdgcn_readfirstlane(L0 + L);
-#pragma unroll
-    for (int u = 0; u < EPR; ++u) {
-      fa[u] = lf[Lb + u];
-      ma[u] = lm[Lb + u];
-    }
-  };
-  const uint32_t hi = (A.dbg & 64u) ? 0u : nl;
-  if (hi) maps(0);
-  for (uint32_t q = lane; q < nne; q += 64) nb[q] = A.nebase[ne0 + q];
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint64_t lbits = (2ull << lane) - 2ull;
-  typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
-  double va[EPR], vb[EPR];
-  uint32_t ra[EPR], rbuf[EPR];
-  auto issue = [&](uint32_t L, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
-#pragma unroll
-    for (int u = 0; u < EPR; ++u) {
-      const uint32_t i = (L + u) * 64u + static_cast<uint32_t>(lane);
-      const uint32_t q = fa[u] + static_cast<uint32_t>(__popcll(ma[u] & lbits));
-      const uint32_t pc = (L + u < hi && i < tot) ? nb[q] + i : 0u;
-      vv[u] = A.partial[pc];
-    }
-    const u16x8 r8 = *reinterpret_cast<const u16x8*>(
-        A.roffL + ((static_cast<uint64_t>(G0 + L / EPR) * 64u) + static_cast<uint32_t>(lane)) * EPR);
-#pragma unroll
-    for (int u = 0; u < EPR; ++u) rr[u] = r8[u];
-    maps(L + EPR);
-  };
-  auto add = [&](uint32_t L, const double (&vv)[EPR], const uint32_t (&rr)[EPR]) {
-#pragma unroll
-    for (int u = 0; u < EPR; ++u)
-      if (L + u < hi && (L + u) * 64u + static_cast<uint32_t>(lane) < tot) atomicAdd(&aw[rr[u]], vv[u]);
-  };
-  if (hi) issue(0, va, ra);
-  for (uint32_t L = 0; L < hi; L += 2 * EPR) {
-    const bool n1 = L + EPR < hi, n2 = L + 2 * EPR < hi;
-    if (n1) issue(L + EPR, vb, rbuf);
-    add(L, va, ra);
-    if (n2) issue(L + 2 * EPR, va, ra);
-    if (n1) add(L + EPR, vb, rbuf);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (A.dbg & 32u) return;
-  const double a = A.st->a;
-  for (uint32_t l = static_cast<uint32_t>(lane); l < RB; l += 64) {
-    const uint32_t row = rb0 + l;
-    const bool in = row < rb1;
-    const uint32_t mt = in ? A.meta[row] : 0u;
-    const double ro = (MODE == 2 && in) ? (A.r_old ? A.r_old[row] : A.r0) : 0.0;
-    double c = aw[l];
-    if (A.dbg & 64u) c = 1.0;
-    row_finish<MODE>(A, a, clsB ? 1u : 0u, row, c, in, mt, ro, lw);
-  }
-  if (clsB || MODE == 2) {  // wave-uniform: this wave's record -> one shard
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < REC_WORDS && lw[lane])
-      atomicAdd(reinterpret_cast<unsigned long long*>(
-                    &A.shards[((blockIdx.x * 4u + static_cast<uint32_t>(wv)) % NSHARD) * REC_WORDS + lane]),
-                static_cast<unsigned long long>(lw[lane]));
-  }
-}
-
 // ---- the stream launch: persistent, slice j = blockIdx % 8 (one XCD per slice) ----------
 // Slice j's stream is cut into tasks of TASK = 1024 edges; wave w of the XCD takes tasks
 // w, w + W, w + 2W, ... (W = waves per XCD), so the XCD sweeps the stream front to back and
@@ -2207,19 +2104,6 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
       }
       hgoff[NB] = static_cast<uint32_t>(groups);
       g->n_groups = groups;
-      // light tails (spmv_rows_light): the longest suffix of class A / of class B whose
-      // blocks all have <= LIGHT_LINES lines and <= LIGHT_NS non-empty runs (PR_LIGHT=0: none)
-      auto light = [&](uint32_t bb) {
-        return hloff[bb + 1] - hloff[bb] <= LIGHT_LINES && hneoff[bb + 1] - hneoff[bb] <= LIGHT_NS;
-      };
-      const bool use_light = env_int("PR_LIGHT", 1) != 0;
-      uint32_t la = RBk.nbA, lb = NB;
-      if (use_light) {
-        while (la > RBk.nbH && light(la - 1)) --la;
-        while (lb > RBk.nbA && light(lb - 1)) --lb;
-      }
-      g->row_la = la;
-      g->row_lb = lb;
       TRY(dmalloc(&g->goff, NB + 1ull, err));
       TRY(dmalloc(&g->roffL, std::max<uint64_t>(groups, 1) * 64 * EPR, err));
       HIPTRY(hipMemcpyAsync(g->goff, hgoff.data(), 4ull * (NB + 1), hipMemcpyHostToDevice, s));
@@ -2427,31 +2311,14 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
   A.rank = static_cast<uint32_t>(g->rank);
   A.sm = g->sm ? 1u : 0u;
   A.SL = g->SL;
+  A.b0 = b0;
   A.xg = std::max(1u, g->tune.rxg);
-  // the range splits into its class-A and class-B parts; each part's light tail (class A
-  // from row_la, class B from row_lb) runs one wave per block (spmv_rows_light), the rest one
-  // workgroup per block
-  const uint32_t nbA = g->nb_rows_a;
-  const uint32_t parts[2][3] = {{b0, std::min(b1, nbA), g->row_la},
-                                {std::max(b0, nbA), b1, g->row_lb}};
-  for (const auto& pt : parts) {
-    const uint32_t lo = pt[0], hi = pt[1];
-    if (hi <= lo) continue;
-    const uint32_t bn = std::min(hi, std::max(lo, pt[2]));  // [lo, bn) normal, [bn, hi) light
-    A.b0 = lo;
-    A.xfull = (bn - lo) / (NSLICE * A.xg) * (NSLICE * A.xg);
-    if (bn > lo) {
-      const dim3 gr(bn - lo), bl(BLOCK);
-      if (mode == 0) hipLaunchKernelGGL((spmv_rows<0>), gr, bl, 0, s, A);
-      else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1>), gr, bl, 0, s, A);
-      else hipLaunchKernelGGL((spmv_rows<2>), gr, bl, 0, s, A);
-    }
-    if (hi > bn) {
-      const dim3 gr((hi - bn + 3) / 4), bl(BLOCK);
-      if (mode == 0) hipLaunchKernelGGL((spmv_rows_light<0>), gr, bl, 0, s, A, bn, hi);
-      else if (mode == 1) hipLaunchKernelGGL((spmv_rows_light<1>), gr, bl, 0, s, A, bn, hi);
-      else hipLaunchKernelGGL((spmv_rows_light<2>), gr, bl, 0, s, A, bn, hi);
-    }
+  A.xfull = (b1 - b0) / (NSLICE * A.xg) * (NSLICE * A.xg);
+  if (b1 > b0) {
+    const dim3 gr(b1 - b0), bl(BLOCK);
+    if (mode == 0) hipLaunchKernelGGL((spmv_rows<0>), gr, bl, 0, s, A);
+    else if (mode == 1) hipLaunchKernelGGL((spmv_rows<1>), gr, bl, 0, s, A);
+    else hipLaunchKernelGGL((spmv_rows<2>), gr, bl, 0, s, A);
   }
   HIPTRY(hipGetLastError());
   return PR_OK;
