@@ -29,8 +29,10 @@ for c in range(cases):
     env = dict(os.environ)
     if rng.random() < 0.6:  # tiny stream geometry: every code path at small scale
         env.update(PR_HOTLDS=str(rng.choice([64, 256, 1024, 4096])), PR_NLDS=str(rng.randint(0, 20)),
-                   PR_QH=str(rng.choice([256, 1024, 8192])), PR_SEG=str(rng.choice([128, 512, 4096])))
-    geo = " ".join(f"{k}={env[k]}" for k in ("PR_HOTLDS", "PR_NLDS", "PR_QH", "PR_SEG") if k in env)
+                   PR_QH=str(rng.choice([256, 1024, 8192])), PR_SEG=str(rng.choice([128, 512, 4096])),
+                   PR_L2W=str(rng.choice([0, 2, 4, 7])), PR_RXG=str(rng.choice([1, 2, 16])))
+    geo = " ".join(f"{k}={env[k]}" for k in ("PR_HOTLDS", "PR_NLDS", "PR_QH", "PR_SEG", "PR_L2W", "PR_RXG")
+                   if k in env)
     src = CASE % dict(root=ROOT, scale=scale, ef=ef, seed=seed, p=p, T=T)
     r = subprocess.run([sys.executable, "-c", src], env=env, capture_output=True, text=True, timeout=300)
     tag = f"case {c}: scale {scale} ef {ef} seed {seed} p {p} T {T} {geo}"
