@@ -596,8 +596,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
     if constexpr ((NTC & 4) != 0) bnx = __builtin_nontemporal_load(bits + so / EPL);
     else bnx = bits[so / EPL];
-    if (A.dbg & 256u) tpn = A.task_piece[tt];  // A/B switch: vector load
-    else tpn = tpa[static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(tt)))];
+    tpn = tpa[static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(tt)))];
   };
   // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
   // with 1/nlds of the L2 part's tasks (LDS-bound and L2-bound work side by side); with no
