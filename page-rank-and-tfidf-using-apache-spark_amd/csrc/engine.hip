@@ -559,9 +559,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   const uint32_t* __restrict__ col = A.col;
   const uint16_t* __restrict__ col16 = A.col16;
   const uint16_t* __restrict__ bits = A.bits;
-  // first piece of a task: wave-uniform, so a scalar load (constant address space)
-  const __attribute__((address_space(4))) uint32_t* tpa =
-      (const __attribute__((address_space(4))) uint32_t*)(A.task_piece);
+  const uint32_t* __restrict__ tpa = A.task_piece;
   double* __restrict__ part = A.partial;
   const uint32_t cm = A.colmask;
   const uint32_t ngs = A.nlds + 1;
@@ -596,7 +594,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     const uint64_t so = static_cast<uint64_t>(tt) * TASK + lane * EPL;
     if constexpr ((NTC & 4) != 0) bnx = __builtin_nontemporal_load(bits + so / EPL);
     else bnx = bits[so / EPL];
-    tpn = tpa[static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(tt)))];
+    tpn = tpa[tt];
   };
   // Phases: phase gi < nlds holds LDS block gi and sweeps that block's tasks interleaved
   // with 1/nlds of the L2 part's tasks (LDS-bound and L2-bound work side by side); with no
