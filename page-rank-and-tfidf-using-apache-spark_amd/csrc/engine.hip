@@ -2273,6 +2273,23 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
               gi, st_avg, end_avg, end_max, span_avg, st_avg - prev_end, (unsigned long long)lt, (unsigned long long)l2t);
       prev_end = end_avg;
     }
+    // per slice (= XCD): tasks and when its workgroups finish (the launch's tail)
+    const uint32_t ngs = g->nlds + 1;
+    for (int j = 0; j < NSLICE; ++j) {
+      double e_avg = 0, e_max = 0, e_min = 1e30;
+      int cnt = 0;
+      for (uint32_t b = static_cast<uint32_t>(j); b < nwg; b += NSLICE) {
+        uint64_t e = 0;
+        for (uint32_t gi = 0; gi < nph; ++gi)
+          for (int w = 1; w <= 16; ++w) e = std::max(e, hst[(static_cast<size_t>(b) * nph + gi) * 17 + w]);
+        const double et = (e - t0) * 0.01;
+        e_avg += et; e_max = std::max(e_max, et); e_min = std::min(e_min, et); ++cnt;
+      }
+      const uint64_t lds_t = g->gtask[j * ngs + g->nlds] - g->gtask[j * ngs];
+      const uint64_t l2_t = g->gtask[j * ngs + g->nlds + 1] - g->gtask[j * ngs + g->nlds];
+      fprintf(stderr, "[stamps] slice %d: lds tasks %7llu l2 tasks %7llu  workgroup end min %8.1f avg %8.1f max %8.1f us\n",
+              j, (unsigned long long)lds_t, (unsigned long long)l2_t, e_min, e_avg / std::max(cnt, 1), e_max);
+    }
   }
   HIPTRY(hipGetLastError());
   return PR_OK;
