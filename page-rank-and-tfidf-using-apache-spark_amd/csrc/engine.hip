@@ -876,19 +876,9 @@ __global__ void k_make_keys(const uint32_t* src, const uint32_t* dst, uint64_t m
 // digest {sum, xor} of mix64(src<<32|dst): per-block partials into DIGEST_SHARDS shards
 // (single-address atomics from every block serialised this kernel at scale 26).
 constexpr int DIGEST_SHARDS = 4096;
-// out-degree counts of hub sources gather in a per-workgroup LDS table first (direct-mapped,
-// tag claimed by CAS; a lane whose slot holds another source counts in global memory), so the
-// hubs' edges cost LDS atomics instead of contended global ones; the table is flushed once
-constexpr int DEG_SLOTS = 4096;
 __global__ void k_degrees(const uint64_t* uk, uint64_t nnz, int nb, uint32_t* outdeg,
                           uint64_t* run_lo, uint64_t* run_hi, unsigned long long* digest) {
   __shared__ unsigned long long ssum[BLOCK / 64], sxor[BLOCK / 64];
-  __shared__ uint32_t tag[DEG_SLOTS], cntl[DEG_SLOTS];
-  for (int i = threadIdx.x; i < DEG_SLOTS; i += BLOCK) {
-    tag[i] = 0xFFFFFFFFu;
-    cntl[i] = 0;
-  }
-  __syncthreads();
   PRMI_BLOCK_LOOP(nnz) {
     const uint64_t e = blk_ * blockDim.x + threadIdx.x;
     uint64_t h = 0;
@@ -896,11 +886,7 @@ __global__ void k_degrees(const uint64_t* uk, uint64_t nnz, int nb, uint32_t* ou
       const uint64_t k = uk[e];
       const uint32_t d = static_cast<uint32_t>(k >> nb);
       const uint32_t s = static_cast<uint32_t>(k & ((1ull << nb) - 1));
-      const uint32_t slot = static_cast<uint32_t>((static_cast<uint64_t>(s) * 0x9E3779B97F4A7C15ull) >> 52);
-      uint32_t t = tag[slot];
-      if (t == 0xFFFFFFFFu) t = atomicCAS(&tag[slot], 0xFFFFFFFFu, s), t = (t == 0xFFFFFFFFu) ? s : t;
-      if (t == s) atomicAdd(&cntl[slot], 1u);
-      else atomicAdd(&outdeg[s], 1u);
+      atomicAdd(&outdeg[s], 1u);
       if (e == 0 || static_cast<uint32_t>(uk[e - 1] >> nb) != d) run_lo[d] = e;
       if (e + 1 == nnz || static_cast<uint32_t>(uk[e + 1] >> nb) != d) run_hi[d] = e + 1;
       h = mix64((static_cast<uint64_t>(s) << 32) | d);
@@ -928,8 +914,6 @@ __global__ void k_degrees(const uint64_t* uk, uint64_t nnz, int nb, uint32_t* ou
     }
     __syncthreads();  // the next iteration reuses the shared partials
   }
-  for (int i = threadIdx.x; i < DEG_SLOTS; i += BLOCK)
-    if (cntl[i]) atomicAdd(&outdeg[tag[i]], cntl[i]);
 }
 
 __global__ void k_indeg_from_runs(const uint64_t* run_lo, const uint64_t* run_hi, uint32_t n,
