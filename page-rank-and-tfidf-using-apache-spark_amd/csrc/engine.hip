@@ -740,26 +740,11 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (A.dbg & 512u) {  // A/B: one row at a time
+      if (!(A.dbg & 1u))
         for (uint32_t i = lane; i < wn; i += 64) {
           if constexpr (NT >= 2) __builtin_nontemporal_store(stg[i], part + tp0 + w0 + i);
           else part[tp0 + w0 + i] = stg[i];
         }
-      } else if (!(A.dbg & 1u)) {
-        // window reads two rows at a time, then their stores (one LDS wait per 128 pieces)
-        static_assert(STG % 128 == 0, "staging window: pairs of wave rows");
-        for (uint32_t i0 = static_cast<uint32_t>(lane); i0 < wn; i0 += 128) {
-          const uint32_t i1 = i0 + 64u;
-          const double s0 = stg[i0], s1 = i1 < wn ? stg[i1] : 0.0;
-          if constexpr (NT >= 2) {
-            __builtin_nontemporal_store(s0, part + tp0 + w0 + i0);
-            if (i1 < wn) __builtin_nontemporal_store(s1, part + tp0 + w0 + i1);
-          } else {
-            part[tp0 + w0 + i0] = s0;
-            if (i1 < wn) part[tp0 + w0 + i1] = s1;
-          }
-        }
-      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
