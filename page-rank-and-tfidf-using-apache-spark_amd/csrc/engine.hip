@@ -2247,17 +2247,23 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
     uint64_t t0 = ~0ull;
     for (uint32_t b = 0; b < nwg; ++b) t0 = std::min<uint64_t>(t0, hst[(static_cast<size_t>(b) * nph) * 17]);
     for (uint32_t gi = 0; gi < nph; ++gi) {
-      double st_avg = 0, end_avg = 0, end_max = 0, span_avg = 0;
+      double st_avg = 0, end_avg = 0, end_max = 0, span_avg = 0, wait_avg = 0;
       for (uint32_t b = 0; b < nwg; ++b) {
         const uint64_t* q = &hst[(static_cast<size_t>(b) * nph + gi) * 17];
         uint64_t e = 0;
         for (int w = 1; w <= 16; ++w) e = std::max(e, q[w]);
+        // barrier wait: how long the LDS waves that finished early wait for the last one
+        double ws = 0;
+        int wn = 0;
+        for (int w = 1; w <= 16; ++w)
+          if (q[w]) { ws += static_cast<double>(e - q[w]); ++wn; }
+        wait_avg += wn ? ws / wn * 0.01 : 0.0;
         st_avg += (q[0] - t0) * 0.01;
         end_avg += (e - t0) * 0.01;
         end_max = std::max(end_max, (e - t0) * 0.01);
         span_avg += (e - q[0]) * 0.01;
       }
-      st_avg /= nwg; end_avg /= nwg; span_avg /= nwg;
+      st_avg /= nwg; end_avg /= nwg; span_avg /= nwg; wait_avg /= nwg;
       uint64_t lt = 0, l2t = 0;  // tasks of the phase over the 8 slices
       const uint32_t ngs = g->nlds + 1;
       for (int j = 0; j < NSLICE; ++j) {
@@ -2269,8 +2275,8 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
           l2t += l2n;
         }
       }
-      fprintf(stderr, "[stamps] phase %2u start %8.1f us  end avg %8.1f max %8.1f  span avg %7.1f  fill+wait %6.1f  lds tasks %7llu  l2 tasks %7llu\n",
-              gi, st_avg, end_avg, end_max, span_avg, st_avg - prev_end, (unsigned long long)lt, (unsigned long long)l2t);
+      fprintf(stderr, "[stamps] phase %2u start %8.1f us  end avg %8.1f max %8.1f  span avg %7.1f  fill+wait %6.1f  wave wait %6.1f  lds tasks %7llu  l2 tasks %7llu\n",
+              gi, st_avg, end_avg, end_max, span_avg, st_avg - prev_end, wait_avg, (unsigned long long)lt, (unsigned long long)l2t);
       prev_end = end_avg;
     }
     // per slice (= XCD): tasks and when its workgroups finish (the launch's tail)
