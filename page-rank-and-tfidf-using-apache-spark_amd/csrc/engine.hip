@@ -412,7 +412,6 @@ struct StreamArgs {
                              // L2 tasks are shared out over the LDS phases, see l2mode)
   uint32_t* claims;          // [8 * (nlds + 1)] per-(slice, group) task counters, zero at launch
                              // (nullptr: static round-robin task order, PR_DYN=0)
-  uint32_t dyn;              // tasks per claim (PR_DYN)
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
@@ -652,29 +651,14 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // task order: each wave claims its next task from the (slice, group) counter one task
     // ahead, so the slice's waves stay on neighbouring tasks and none waits at the phase
     // barrier for a slower sibling; claims == nullptr: static round-robin u = w, w + nw, ...
-    // Claims come in chunks of A.dyn tasks; the next chunk is claimed a whole chunk ahead.
     uint32_t* const cnt = A.claims ? A.claims + j * ngs + gi : nullptr;
-    const uint32_t CH = A.dyn;
     auto claim = [&]() -> uint32_t {
       uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(cnt, CH);
-      return c;  // lane 0 holds it; read when the chunk starts
+      if (lane == 0) c = atomicAdd(cnt, 1u);
+      return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(c)));
     };
-    uint32_t ccur = 0, cnxt = 0, ck = 0;
-    if (cnt) {
-      ccur = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(claim())));
-      cnxt = claim();
-    }
-    auto advance = [&](uint32_t cur) -> uint32_t {  // the task after `cur`
-      if (!cnt) return cur + nw;
-      if (++ck < CH) return ccur + ck;
-      ck = 0;
-      ccur = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(cnxt)));
-      cnxt = ccur < nu ? claim() : 0u;
-      return ccur;
-    };
-    uint32_t u = cnt ? ccur : w;
-    uint32_t un = u < nu ? advance(u) : nu;
+    uint32_t u = cnt ? claim() : w;
+    uint32_t un = cnt ? (u < nu ? claim() : nu) : w + nw;
     if (u < nu) fetch_u(u);
     while (u < nu) {
       const bool lds_task = is_lds(u);
@@ -687,7 +671,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       if (lane == 0) b |= 1u;  // a task always starts a piece
       // next task's stream words first: they stay in flight while this task gathers
       if (un < nu) fetch_u(un);
-      const uint32_t unn = un < nu ? advance(un) : nu;
+      const uint32_t unn = cnt ? (un < nu ? claim() : nu) : un + nw;
       double v[EPL];
       if (lds_task) {
         // every source of an LDS-group task is inside the block (padding reads the zero slot)
@@ -2162,7 +2146,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   if (T.dbg && NP) hipLaunchKernelGGL(k_fill_f64, dim3(grid_loop(NP)), dim3(BLOCK), 0, s, g->partial, NP, 1.0);
 
   span.next("prmi:build:iteration buffers");
-  if (env_int("PR_DYN", 4)) {
+  if (env_int("PR_DYN", 1)) {
     TRY(dmalloc(&g->claims, NSLICE * (g->nlds + 1ull), err));
     HIPTRY(hipMemsetAsync(g->claims, 0, 4ull * NSLICE * (g->nlds + 1), s));
   }
@@ -2275,7 +2259,6 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   S.stamps = dst;
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
   S.claims = g->claims;
-  S.dyn = static_cast<uint32_t>(std::max(1, env_int("PR_DYN", 4)));
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
