@@ -145,7 +145,6 @@ struct DevGraph {
   uint64_t* lmask = nullptr;      // [lines] run starts inside the line
   uint32_t* goff = nullptr;       // [nb_rows + 1] first 8-line group of each block
   uint16_t* roffL = nullptr;      // [groups * 64 * 8] row offsets in row-launch order
-  uint32_t* claims = nullptr;     // [8 * (nlds + 1)] stream-launch task counters (PR_DYN)
   uint32_t* meta = nullptr;
   uint32_t* perm = nullptr;       // internal -> original
   uint32_t* outdeg = nullptr;     // by original id

@@ -410,8 +410,6 @@ struct StreamArgs {
                              // and every wave's end (s_memrealtime, 100 MHz); nullptr = off
   uint32_t l2w;              // PR_L2W: waves per workgroup dedicated to the L2 group (0 = the
                              // L2 tasks are shared out over the LDS phases, see l2mode)
-  uint32_t* claims;          // [8 * (nlds + 1)] per-(slice, group) task counters, zero at launch
-                             // (nullptr: static round-robin task order, PR_DYN=0)
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
@@ -648,19 +646,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       fetch(task_of(u), lt, lt ? tb : l2b, lt ? lbase : l2base);
     };
     const uint32_t nu = nL + nR;
-    // task order: each wave claims its next task from the (slice, group) counter one task
-    // ahead, so the slice's waves stay on neighbouring tasks and none waits at the phase
-    // barrier for a slower sibling; claims == nullptr: static round-robin u = w, w + nw, ...
-    uint32_t* const cnt = A.claims ? A.claims + j * ngs + gi : nullptr;
-    auto claim = [&]() -> uint32_t {
-      uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(cnt, 1u);
-      return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(c)));
-    };
-    uint32_t u = cnt ? claim() : w;
-    uint32_t un = cnt ? (u < nu ? claim() : nu) : w + nw;
-    if (u < nu) fetch_u(u);
-    while (u < nu) {
+    if (w < nu) fetch_u(w);
+    for (uint32_t u = w; u < nu; u += nw) {
       const bool lds_task = is_lds(u);
       u32x4 cv[4];
 #pragma unroll
@@ -670,8 +657,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       if (A.dbg & 4u) b = 0;
       if (lane == 0) b |= 1u;  // a task always starts a piece
       // next task's stream words first: they stay in flight while this task gathers
-      if (un < nu) fetch_u(un);
-      const uint32_t unn = cnt ? (un < nu ? claim() : nu) : un + nw;
+      if (u + nw < nu) fetch_u(u + nw);
       double v[EPL];
       if (lds_task) {
         // every source of an LDS-group task is inside the block (padding reads the zero slot)
@@ -763,18 +749,13 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-      u = un;
-      un = unn;
     }
     if (stp && lane == 0) stp[1 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
 // Sum the NSHARD shards into one record and clear them for the next round.
-__global__ __launch_bounds__(BLOCK) void reduce_shards(uint64_t* shards, uint64_t* rec,
-                                                      uint32_t* claims, uint32_t nclaims) {
-  // the stream launch's task counters, ready for the next round
-  for (uint32_t i = threadIdx.x; i < nclaims; i += BLOCK) claims[i] = 0;
+__global__ __launch_bounds__(BLOCK) void reduce_shards(uint64_t* shards, uint64_t* rec) {
   __shared__ uint64_t part[8][REC_WORDS];
   const int w = threadIdx.x & 31, g = threadIdx.x >> 5;
   uint64_t s = 0;
@@ -1568,7 +1549,7 @@ void dev_free(DevGraph* g) {
   auto F = [](void* p) { if (p) (void)hipFree(p); };
   F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->roff); F(g->runs);
   F(g->nebase); F(g->ne_off); F(g->l_off); F(g->btot); F(g->lfirst); F(g->lmask);
-  F(g->goff); F(g->roffL); F(g->claims);
+  F(g->goff); F(g->roffL);
   F(g->d_gtask); F(g->d_gstart); F(g->d_gbase); F(g->col16);
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
@@ -2146,10 +2127,6 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   if (T.dbg && NP) hipLaunchKernelGGL(k_fill_f64, dim3(grid_loop(NP)), dim3(BLOCK), 0, s, g->partial, NP, 1.0);
 
   span.next("prmi:build:iteration buffers");
-  if (env_int("PR_DYN", 1)) {
-    TRY(dmalloc(&g->claims, NSLICE * (g->nlds + 1ull), err));
-    HIPTRY(hipMemsetAsync(g->claims, 0, 4ull * NSLICE * (g->nlds + 1), s));
-  }
   // ---- iteration buffers ----------------------------------------------------------------
   TRY(dmalloc(&g->r_loc[0], lrows, err));
   TRY(dmalloc(&g->r_loc[1], lrows, err));
@@ -2180,7 +2157,6 @@ int dev_reset_state(DevGraph* g, hipStream_t s) {
   }
   HIPTRY(hipMemcpyAsync(g->state, &st, sizeof(st), hipMemcpyHostToDevice, s));
   HIPTRY(hipMemsetAsync(g->shards, 0, 8ull * NSHARD * REC_WORDS, s));
-  if (g->claims) HIPTRY(hipMemsetAsync(g->claims, 0, 4ull * NSLICE * (g->nlds + 1), s));
   return PR_OK;
 }
 
@@ -2258,7 +2234,6 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   }
   S.stamps = dst;
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
-  S.claims = g->claims;
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
@@ -2375,8 +2350,7 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
 int dev_round_reduce(DevGraph* g, hipStream_t s, hipEvent_t ev1) {
   std::string* err = nullptr;
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
-  hipLaunchKernelGGL(reduce_shards, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local, g->claims,
-                     g->claims ? static_cast<uint32_t>(NSLICE * (g->nlds + 1)) : 0u);
+  hipLaunchKernelGGL(reduce_shards, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local);
   HIPTRY(hipGetLastError());
   return PR_OK;
 }
