@@ -27,6 +27,9 @@ import prmi355x as P  # noqa: E402
 P.lib()  # load the engine (and ROCm's HIP + RCCL) before torch brings its own copies
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+# achievable streaming-read bandwidth measured on the box (8 x dwordx4 per lane, 1 WG/CU;
+# profiles/r01/stream_probe.log, scripts/probes/): SURVEY.md 8d's "STREAM-copy" reference
+STREAM_READ_GBS = 6330.0
 
 
 def parse():
@@ -168,7 +171,9 @@ def main():
                                         "launches of each round, mean over the timed rounds "
                                         "(pr_stats.ms_spmv_kernel)",
                          "kernel_ms": round(kms, 4),
-                         "algorithmic_bytes_per_launch": bytes_launch},
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "achievable_stream_read_gbs": STREAM_READ_GBS,
+                         "frac_of_achievable": round(achieved / STREAM_READ_GBS, 4)},
             "cpu_baseline": cpu,
             "device_ms_per_round": round(st["ms_per_iter"], 4),
             "build_s": round(build_s, 2),
