@@ -1936,6 +1936,11 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     g->n_pieces = np;
     g->n_pairs = 0;
     for (unsigned long long v : hp) g->n_pairs += v;
+    // pieces <= pairs + tasks (a task boundary cuts at most one pair); piece indices are u32
+    if (g->n_pairs + tasks > 0xFFFFFFFFull) {
+      if (err) *err = "too many pieces for one rank (use more ranks)";
+      return PR_E_ARG;
+    }
   }
   const uint64_t NP = g->n_pieces;
   span.next("prmi:build:row maps");
