@@ -176,6 +176,10 @@ def main():
                          "frac_of_achievable": round(achieved / STREAM_READ_GBS, 4)},
             "cpu_baseline": cpu,
             "device_ms_per_round": round(st["ms_per_iter"], 4),
+            # per round: the SpMV launches (slowest rank) and what the exchange, the record
+            # all-gather and finalize leave exposed on top of them
+            "round_breakdown_ms": {"spmv_kernels": round(kms, 4),
+                                   "exposed_exchange_and_finalize": round(max(ms_step - kms, 0.0), 4)},
             "build_s": round(build_s, 2),
             "build_id": P.build_id(),
         }
