@@ -410,6 +410,8 @@ struct StreamArgs {
                              // and every wave's end (s_memrealtime, 100 MHz); nullptr = off
   uint32_t l2w;              // PR_L2W: waves per workgroup dedicated to the L2 group (0 = the
                              // L2 tasks are shared out over the LDS phases, see l2mode)
+  uint32_t wgdyn;            // PR_WGDYN: LDS waves claim their workgroup's tasks from an LDS
+                             // counter (1) or take them round-robin (0)
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
@@ -534,6 +536,12 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // the barrier counter lives in the spare words after the LDS block's zero slot (the dynamic
   // LDS request is already the whole 160 KiB: no static __shared__ may be added)
   uint32_t& bar_cnt = *reinterpret_cast<uint32_t*>(hot + A.H + 1);
+  // with split roles, a phase's LDS tasks are dealt to the slice's workgroups round-robin
+  // (task u to workgroup u mod 32) and the workgroup's LDS waves claim its tasks from this
+  // counter, so no wave idles at the phase barrier while a sibling still has a backlog
+  uint32_t& task_cnt = *reinterpret_cast<uint32_t*>(hot + A.H + 2);
+  const bool wgdyn = split && !l2role && A.wgdyn != 0u;
+  const uint32_t qwg = blockIdx.x / NSLICE, nqwg = gridDim.x / NSLICE;
   uint32_t bar_gen = 0;
   if (split) {
     if (threadIdx.x == 0) bar_cnt = 0;
@@ -627,6 +635,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (threadIdx.x == 0) hot[A.H] = 0.0;  // the padding column
       }
+      if (threadIdx.x == 0) task_cnt = 0;  // (wave 0 is an LDS wave)
       block_barrier();
     }
     uint64_t* stp = STAMPS ? A.stamps + (static_cast<uint64_t>(blockIdx.x) * nph + gi) * 17u : nullptr;
@@ -646,8 +655,16 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       fetch(task_of(u), lt, lt ? tb : l2b, lt ? lbase : l2base);
     };
     const uint32_t nu = nL + nR;
-    if (w < nu) fetch_u(w);
-    for (uint32_t u = w; u < nu; u += nw) {
+    auto claim = [&]() -> uint32_t {
+      uint32_t m = 0;
+      if (lane == 0) m = atomicAdd(&task_cnt, 1u);
+      return qwg + nqwg * static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
+    };
+    const bool dyn = wgdyn && gi < A.nlds;
+    uint32_t u = dyn ? claim() : w;
+    uint32_t un = dyn ? (u < nu ? claim() : nu) : w + nw;
+    if (u < nu) fetch_u(u);
+    while (u < nu) {
       const bool lds_task = is_lds(u);
       u32x4 cv[4];
 #pragma unroll
@@ -657,7 +674,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       if (A.dbg & 4u) b = 0;
       if (lane == 0) b |= 1u;  // a task always starts a piece
       // next task's stream words first: they stay in flight while this task gathers
-      if (u + nw < nu) fetch_u(u + nw);
+      if (un < nu) fetch_u(un);
+      const uint32_t unn = dyn ? (un < nu ? claim() : nu) : un + nw;
       double v[EPL];
       if (lds_task) {
         // every source of an LDS-group task is inside the block (padding reads the zero slot)
@@ -749,6 +767,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+      u = un;
+      un = unn;
     }
     if (stp && lane == 0) stp[1 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
   }
@@ -2239,6 +2259,7 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   }
   S.stamps = dst;
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
+  S.wgdyn = static_cast<uint32_t>(env_int("PR_WGDYN", 1) != 0);
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
