@@ -80,7 +80,8 @@ struct Tuning {
   uint32_t rb_heavy = 256;  // PR_RBH: rows per heavy row-launch block
   uint32_t rxg = 16;     // PR_RXG: consecutive row-launch blocks per XCD (1 = round-robin)
   uint32_t heavy_deg = 128; // PR_HDEG: rows with in-degree >= this get heavy blocks (0 = none)
-  int nlds = 18;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill)
+  int nlds = 20;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill; 18
+                        // before the workgroup task claims, 20 with them: +2 %, interleaved runs)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
   // PR_NT: 2 = non-temporal piece stores (they stop evicting x from the L2s: +3 %), 0 =
   // regular stores.  Non-temporal stream loads and LDS fills were measured slower.
