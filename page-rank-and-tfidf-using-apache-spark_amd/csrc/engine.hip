@@ -411,8 +411,7 @@ struct StreamArgs {
   uint32_t l2w;              // PR_L2W: waves per workgroup dedicated to the L2 group (0 = the
                              // L2 tasks are shared out over the LDS phases, see l2mode)
   uint32_t wgdyn;            // PR_WGDYN: LDS waves claim their workgroup's tasks from an LDS
-                             // counter (1; 3: the L2 waves too, from their own) or take them
-                             // round-robin (0)
+                             // counter (1) or take them round-robin (0)
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
@@ -541,12 +540,11 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // (task u to workgroup u mod 32) and the workgroup's LDS waves claim its tasks from this
   // counter, so no wave idles at the phase barrier while a sibling still has a backlog
   uint32_t& task_cnt = *reinterpret_cast<uint32_t*>(hot + A.H + 2);
-  uint32_t& l2_cnt = *reinterpret_cast<uint32_t*>(hot + A.H + 3);  // the L2 waves' counter
-  const bool wgdyn = split && A.wgdyn != 0u && (!l2role || (A.wgdyn & 2u));
+  const bool wgdyn = split && !l2role && A.wgdyn != 0u;
   const uint32_t qwg = blockIdx.x / NSLICE, nqwg = gridDim.x / NSLICE;
   uint32_t bar_gen = 0;
   if (split) {
-    if (threadIdx.x == 0) bar_cnt = l2_cnt = 0;
+    if (threadIdx.x == 0) bar_cnt = 0;
     __syncthreads();
   }
   auto block_barrier = [&]() {
@@ -657,13 +655,12 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       fetch(task_of(u), lt, lt ? tb : l2b, lt ? lbase : l2base);
     };
     const uint32_t nu = nL + nR;
-    uint32_t& my_cnt = l2role ? l2_cnt : task_cnt;
     auto claim = [&]() -> uint32_t {
       uint32_t m = 0;
-      if (lane == 0) m = atomicAdd(&my_cnt, 1u);
+      if (lane == 0) m = atomicAdd(&task_cnt, 1u);
       return qwg + nqwg * static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
     };
-    const bool dyn = wgdyn && (gi < A.nlds || l2role);
+    const bool dyn = wgdyn && gi < A.nlds;
     uint32_t u = dyn ? claim() : w;
     uint32_t un = dyn ? (u < nu ? claim() : nu) : w + nw;
     if (u < nu) fetch_u(u);
@@ -2262,7 +2259,7 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   }
   S.stamps = dst;
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
-  S.wgdyn = static_cast<uint32_t>(env_int("PR_WGDYN", 1));  // 1: LDS waves, 3: L2 waves too
+  S.wgdyn = static_cast<uint32_t>(env_int("PR_WGDYN", 1) != 0);
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
