@@ -104,6 +104,7 @@ struct DevGraph {
   uint32_t nA = 0, nB = 0, nC = 0, nD = 0, R = 0;
   uint32_t maxA = 0;              // x slot length per rank
   bool sm = false;                // slice-major x layout (p divides 8)
+  bool snake = false;             // snake chunk -> slice order (single rank, engine.hip chunk_slice)
   uint32_t SL = 0, SLC = 0;       // slice region lengths (class A / class C)
   uint64_t X = 0;                 // x length
   uint32_t lrows = 0, lA = 0;

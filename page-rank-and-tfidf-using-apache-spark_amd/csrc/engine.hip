@@ -194,6 +194,7 @@ struct RowArgs {
   const IterState* st;
   uint64_t* shards;
   uint32_t p, rank, sm, SL;  // x layout: where local row l's x' goes inside this rank's slot
+  uint32_t snake;            // snake chunk -> slice order (chunk_slice)
   uint32_t dbg;              // PR_DBG timing experiments: 16 no LDS adds, 32 no epilogue, 64 no
                              // pieces; 128 non-temporal piece loads (not timing-only)
   double base, r0;           // damping base (0.15) and initial rank (1.0), or their /N_tot forms
@@ -201,10 +202,22 @@ struct RowArgs {
   uint32_t xg, xfull;        // XCD groups: xg consecutive blocks per XCD in the first xfull
 };
 
+// chunk c (16 columns) -> slice.  Snake order (single rank): c mod 8, reversed in every odd
+// group of 8, so the hottest chunk of a group alternates between slice 0 and slice 7 and no
+// slice systematically receives the hotter half (chunks are in-degree ordered).  With p > 1
+// plain c mod 8, which keeps each rank's chunks in its own slices.
+__device__ __host__ __forceinline__ uint32_t chunk_slice(uint32_t c, uint32_t snake) {
+  const uint32_t sl = c % NSLICE;
+  return (snake && ((c / NSLICE) & 1u)) ? NSLICE - 1 - sl : sl;
+}
+// the chunk of slice sl in group g (inverse of chunk_slice)
+__device__ __host__ __forceinline__ uint32_t slice_chunk(uint32_t g, uint32_t sl, uint32_t snake) {
+  return g * NSLICE + ((snake && (g & 1u)) ? NSLICE - 1 - sl : sl);
+}
 // offset of local row l's x entry inside this rank's slot (see Layout / xpos)
 __device__ __forceinline__ uint32_t xslot_of(const RowArgs& A, uint32_t l) {
   if (!A.sm) return l;
-  const uint32_t c = (l / CHUNK) * A.p + A.rank, sl = c % NSLICE;
+  const uint32_t c = (l / CHUNK) * A.p + A.rank, sl = chunk_slice(c, A.snake);
   return (sl / A.p) * A.SL + (c / NSLICE) * CHUNK + (l % CHUNK);
 }
 
@@ -984,6 +997,7 @@ struct Layout {
   uint32_t p, rank, nA, R, nC, maxA;
   uint32_t sm;        // slice-major x (p divides 8): every slice is one contiguous region
   uint32_t SL, SLC;   // entries per slice region: class-A part / class-C part
+  uint32_t snake;     // snake chunk -> slice order (chunk_slice; single rank only)
 };
 __device__ __host__ __forceinline__ uint32_t owner_of(const Layout& L, uint32_t k) {
   return (k / CHUNK) % L.p;
@@ -1001,17 +1015,17 @@ __device__ __host__ __forceinline__ uint32_t row_of(const Layout& L, uint32_t l)
 __device__ __forceinline__ uint32_t xpos(const Layout& L, uint32_t k) {
   if (k < L.nA) {
     if (!L.sm) return owner_of(L, k) * L.maxA + local_of(L, k);
-    const uint32_t c = k / CHUNK, sl = c % NSLICE;
+    const uint32_t c = k / CHUNK, sl = chunk_slice(c, L.snake);
     return (sl % L.p) * L.maxA + (sl / L.p) * L.SL + (c / NSLICE) * CHUNK + (k % CHUNK);
   }
   const uint32_t kc = k - L.R;
   if (!L.sm) return L.p * L.maxA + kc;
   const uint32_t c = kc / CHUNK;
-  return L.p * L.maxA + (c % NSLICE) * L.SLC + (c / NSLICE) * CHUNK + (kc % CHUNK);
+  return L.p * L.maxA + chunk_slice(c, L.snake) * L.SLC + (c / NSLICE) * CHUNK + (kc % CHUNK);
 }
 // slice of a column = its 128-byte chunk index mod 8 (independent of the rank count)
 __device__ __forceinline__ uint32_t slice_of(const Layout& L, uint32_t k) {
-  return ((k < L.nA ? k : k - L.R) / CHUNK) % NSLICE;
+  return chunk_slice((k < L.nA ? k : k - L.R) / CHUNK, L.snake);
 }
 
 // x of every column from r^0 (r0 on all sources) or, for a seed, from ranks by original id
@@ -1072,19 +1086,19 @@ __device__ __forceinline__ void col_slice_q(const Layout& L, const StreamGeo& G,
                                             uint32_t& sl, uint32_t& q) {
   if (k < L.nA) {
     const uint32_t c = k / CHUNK;
-    sl = c % NSLICE;
+    sl = chunk_slice(c, L.snake);
     q = (c / NSLICE) * CHUNK + k % CHUNK;
   } else {
     const uint32_t kc = k - L.R, c = kc / CHUNK;
-    sl = c % NSLICE;
+    sl = chunk_slice(c, L.snake);
     q = G.SLq + (c / NSLICE) * CHUNK + kc % CHUNK;
   }
 }
 __device__ __forceinline__ uint32_t col_of_slice_q(const Layout& L, const StreamGeo& G,
                                                    uint32_t sl, uint32_t q) {
-  if (q < G.SLq) return ((q / CHUNK) * NSLICE + sl) * CHUNK + q % CHUNK;
+  if (q < G.SLq) return slice_chunk(q / CHUNK, sl, L.snake) * CHUNK + q % CHUNK;
   const uint32_t qc = q - G.SLq;
-  return L.R + ((qc / CHUNK) * NSLICE + sl) * CHUNK + qc % CHUNK;
+  return L.R + slice_chunk(qc / CHUNK, sl, L.snake) * CHUNK + qc % CHUNK;
 }
 __device__ __forceinline__ void seg_of_q(const StreamGeo& G, uint32_t q, uint32_t& seg,
                                          uint32_t& qin) {
@@ -1117,12 +1131,12 @@ __device__ __forceinline__ uint32_t col_of_xpos(const Layout& L, uint32_t x) {
     const uint32_t r = x / L.maxA, y = x % L.maxA;
     if (!L.sm) return ((y / CHUNK) * L.p + r) * CHUNK + y % CHUNK;
     const uint32_t sl = (y / L.SL) * L.p + r, rem = y % L.SL;
-    return ((rem / CHUNK) * NSLICE + sl) * CHUNK + rem % CHUNK;
+    return slice_chunk(rem / CHUNK, sl, L.snake) * CHUNK + rem % CHUNK;
   }
   const uint32_t qc = x - PA;
   if (!L.sm) return L.R + qc;
   const uint32_t sl = qc / L.SLC, rem = qc % L.SLC;
-  return L.R + ((rem / CHUNK) * NSLICE + sl) * CHUNK + rem % CHUNK;
+  return L.R + slice_chunk(rem / CHUNK, sl, L.snake) * CHUNK + rem % CHUNK;
 }
 
 // relabel unique edges to stream keys (slice, segment, local row, q within segment); with p > 1
@@ -1585,7 +1599,7 @@ namespace {
 
 Layout layout_of(const DevGraph* g) {
   return Layout{static_cast<uint32_t>(g->p), static_cast<uint32_t>(g->rank), g->nA, g->R, g->nC,
-                g->maxA, g->sm ? 1u : 0u, g->SL, g->SLC};
+                g->maxA, g->sm ? 1u : 0u, g->SL, g->SLC, g->snake ? 1u : 0u};
 }
 
 // rows owned by rank j among internal ids [0, cnt) when chunks of CHUNK are dealt round-robin
@@ -1786,6 +1800,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   g->R = g->nA + g->nB;
   const uint32_t P = static_cast<uint32_t>(p), RK = static_cast<uint32_t>(rank);
   g->sm = (NSLICE % P) == 0 && env_int("PR_SLICE_MAJOR", 1) != 0;
+  g->snake = g->sm && P == 1 && env_int("PR_SNAKE", 1) != 0;
   if (g->sm) {
     const uint32_t chA = (g->nA + CHUNK - 1) / CHUNK, chC = (g->nC + CHUNK - 1) / CHUNK;
     g->SL = CHUNK * ((chA + NSLICE - 1) / NSLICE);
@@ -2359,6 +2374,7 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
   A.p = static_cast<uint32_t>(g->p);
   A.rank = static_cast<uint32_t>(g->rank);
   A.sm = g->sm ? 1u : 0u;
+  A.snake = g->snake ? 1u : 0u;
   A.SL = g->SL;
   A.b0 = b0;
   A.xg = std::max(1u, g->tune.rxg);
