@@ -94,6 +94,10 @@ struct Tuning {
   int l2w = 4;          // PR_L2W: waves per stream workgroup dedicated to the L2 group
                         // (of 16; 0 = L2 tasks shared out over the LDS phases as in round 1;
                         // 2/3/4/5/6/8 measured at scale 26, 3-4 best)
+  int lean = 1;         // PR_LEAN: 1 = the lean per-task instruction stream of the stream launch
+                        // (fma-form piece sums, DPP-masked scans, SDWA LDS addresses: -11 %
+                        // VALU instructions, time unchanged), 0 = the earlier form; both
+                        // produce bit-identical sums
 };
 
 struct DevGraph {

@@ -483,6 +483,66 @@ __device__ __forceinline__ double wave_seg_scan(double S, int F, int lane) {
   return S;
 }
 
+// ---- lean forms (the LEAN stream variant): the same sums in the same order, fewer VALU ops.
+// The scan steps need no per-lane conditions: row shifts zero-fill the lanes whose source lies
+// outside the row (bound_ctrl), and the row broadcasts only write the rows that take them
+// (row mask 0xA / 0xC; the other rows keep the zero `old`).  A lane that reads zero adds
+// nothing: S + 0 = S, F | 0 = F.
+template <int CTRL>
+__device__ __forceinline__ int dppz_i(int v) {
+  if constexpr (CTRL == DPP_ROW_BCAST15) return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xA, 0xF, false);
+  else if constexpr (CTRL == DPP_ROW_BCAST31) return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xC, 0xF, false);
+  else return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ double dppz_d(double v) {
+  const uint64_t u = static_cast<uint64_t>(__double_as_longlong(v));
+  const uint32_t lo = static_cast<uint32_t>(dppz_i<CTRL>(static_cast<int>(u)));
+  const uint32_t hi = static_cast<uint32_t>(dppz_i<CTRL>(static_cast<int>(u >> 32)));
+  return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(hi) << 32) | lo));
+}
+__device__ __forceinline__ int wave_incl_scan_lean(int v) {
+  v += dppz_i<DPP_ROW_SHR1>(v);
+  v += dppz_i<DPP_ROW_SHR2>(v);
+  v += dppz_i<DPP_ROW_SHR4>(v);
+  v += dppz_i<DPP_ROW_SHR8>(v);
+  v += dppz_i<DPP_ROW_BCAST15>(v);
+  v += dppz_i<DPP_ROW_BCAST31>(v);
+  return v;
+}
+// the segmented scan of wave_seg_scan with the combine S = F ? S : Su + S written as
+// fma(Su, !F, S): for !F = 1 that is the correctly rounded Su + S, for !F = 0 exactly S
+__device__ __forceinline__ double wave_seg_scan_lean(double S, int F) {
+#define PRMI_SEG_STEP_L(CTRL)                                                   \
+  {                                                                             \
+    const double Su = dppz_d<CTRL>(S);                                          \
+    const int Fu = dppz_i<CTRL>(F);                                             \
+    S = __builtin_fma(Su, static_cast<double>(static_cast<uint32_t>(F ^ 1)), S); \
+    F |= Fu;                                                                    \
+  }
+  PRMI_SEG_STEP_L(DPP_ROW_SHR1)
+  PRMI_SEG_STEP_L(DPP_ROW_SHR2)
+  PRMI_SEG_STEP_L(DPP_ROW_SHR4)
+  PRMI_SEG_STEP_L(DPP_ROW_SHR8)
+  PRMI_SEG_STEP_L(DPP_ROW_BCAST15)
+  PRMI_SEG_STEP_L(DPP_ROW_BCAST31)
+#undef PRMI_SEG_STEP_L
+  return S;
+}
+// byte offset (x 8) of the low / high 16-bit half of a word in one SDWA shift
+__device__ __forceinline__ uint32_t lds_off_lo(uint32_t w) {
+  uint32_t r;
+  asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+      : "=v"(r) : "v"(w));
+  return r;
+}
+__device__ __forceinline__ uint32_t lds_off_hi(uint32_t w) {
+  uint32_t r;
+  asm("v_lshlrev_b32_sdwa %0, 3, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+      : "=v"(r) : "v"(w));
+  return r;
+}
+
 // Sixteen exec-masked buffer gathers x[off/8] into v[k] (lanes outside gm[k] keep v[k]),
 // then one s_waitcnt: the asm block ends with its loads landed, so the compiler never sees
 // an in-flight destination.
@@ -529,7 +589,7 @@ __device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[
 // NT: 2 = non-temporal piece stores.  SPLIT: dedicated L2 waves (A.l2w).  STAMPS: PR_STAMPS
 // diagnostics.  The variants are separate instantiations so that the default one carries no
 // register cost for the others.
-template <int NT, bool SPLIT, bool STAMPS, int NTC = 0>
+template <int NT, bool SPLIT, bool STAMPS, int NTC = 0, bool LEAN = false>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
   const uint32_t j = blockIdx.x % NSLICE;
@@ -696,6 +756,14 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
 #pragma unroll
           for (int k = 0; k < EPL; ++k)
             v[k] = __longlong_as_double(static_cast<long long>(cv[k >> 3][(k >> 1) & 3] & 0x3FFFu));
+        } else if constexpr (LEAN) {
+          // one SDWA shift per address (the block starts at LDS byte 0: no static LDS here)
+          const char* hb = reinterpret_cast<const char*>(hot);
+#pragma unroll
+          for (int k = 0; k < EPL; ++k) {
+            const uint32_t wd = cv[k >> 3][(k >> 1) & 3];
+            v[k] = *reinterpret_cast<const double*>(hb + ((k & 1) ? lds_off_hi(wd) : lds_off_lo(wd)));
+          }
         } else {
 #pragma unroll
           for (int k = 0; k < EPL; ++k) {
@@ -723,7 +791,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       }
     // exclusive prefix (over lanes) of the piece starts -> first piece index of this lane
     const int cnt = __popc(b);
-    const int C = wave_incl_scan(cnt, lane);
+    const int C = LEAN ? wave_incl_scan_lean(cnt) : wave_incl_scan(cnt, lane);
     const uint32_t first = static_cast<uint32_t>(C - cnt);  // task-relative index of the lane's first start
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(C, 63));  // pieces of the task
     // one pass over the lane's edges: pv[k] = the running sum just before edge k (for a start
@@ -732,14 +800,30 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // a plain left-to-right sum per piece.
     double run = 0.0;
     double pv[EPL];
+    double S;
+    if constexpr (LEAN) {
+      // run = start ? v : run + v as fma(run, !start, v): exactly v, or the correctly rounded
+      // run + v (three ops per edge: bit extract, convert, fma)
+      const uint32_t nb = ~b;
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      pv[k] = run;
-      const double t = run + v[k];
-      run = ((b >> k) & 1u) ? v[k] : t;
+      for (int k = 0; k < EPL; ++k) {
+        pv[k] = run;
+        run = __builtin_fma(run, static_cast<double>((nb >> k) & 1u), v[k]);
+      }
+      // the segmented scan only matters when some lane holds no start (a piece crossing a
+      // whole lane); otherwise every lane's inclusive value is its own open piece
+      if (__builtin_amdgcn_ballot_w64(b == 0u) == 0ull) S = run;
+      else S = wave_seg_scan_lean(run, b != 0u ? 1 : 0);
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        pv[k] = run;
+        const double t = run + v[k];
+        run = ((b >> k) & 1u) ? v[k] : t;
+      }
+      // segmented inclusive scan of the open piece over lanes (flag: lane holds a start)
+      S = wave_seg_scan(run, b != 0u ? 1 : 0, lane);
     }
-    // segmented inclusive scan of the open piece over lanes (flag: lane holds a start)
-    const double S = wave_seg_scan(run, b != 0u ? 1 : 0, lane);
     const double carry = dpp_d<DPP_WAVE_SHR1>(S);
     const uint32_t bn = static_cast<uint32_t>(dpp_i<DPP_WAVE_SHL1>(static_cast<int>(b)));
     const bool closes = lane == 63 || (bn & 1u) != 0u;  // next edge starts a piece
@@ -1626,6 +1710,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.nt = env_int("PR_NT", T.nt);
   T.hot_lds = static_cast<uint32_t>(std::max(0, std::min(20480, env_int("PR_HOTLDS", static_cast<int>(T.hot_lds)))));
   T.dbg = env_int("PR_DBG", 0);
+  T.lean = env_int("PR_LEAN", T.lean);
   T.rb_heavy = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RBH", static_cast<int>(T.rb_heavy)))));
   T.heavy_deg = static_cast<uint32_t>(std::max(0, env_int("PR_HDEG", static_cast<int>(T.heavy_deg))));
   T.rb = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RB", static_cast<int>(T.rb)))));
@@ -2055,6 +2140,29 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
                 1u << b, b >= 31 ? 0xFFFFFFFFu : (2u << b), hr[b], e, pc, e ? double(pc) / e : 0.0,
                 hh[b * 6 + 1], hh[b * 6 + 0], hh[b * 6 + 3], hh[b * 6 + 2], hh[b * 6 + 5], hh[b * 6 + 4]);
       }
+      // pieces per task, LDS-block tasks vs L2-group tasks: the stream launch stages a task's
+      // pieces through a 256-piece window, one pass per started window
+      std::vector<uint32_t> tp(g->ntask + 1);
+      HIPTRY(hipMemcpyAsync(tp.data(), g->task_piece, 4ull * tp.size(), hipMemcpyDeviceToHost, s));
+      HIPTRY(hipStreamSynchronize(s));
+      const uint32_t ngs = g->nlds + 1;
+      for (int kind = 0; kind < 2; ++kind) {
+        unsigned long long hist8[9] = {0}, nt = 0, np = 0, passes = 0;
+        for (int j = 0; j < NSLICE; ++j)
+          for (uint32_t gi = kind ? g->nlds : 0; gi < (kind ? ngs : g->nlds); ++gi)
+            for (uint32_t t = g->gtask[j * ngs + gi]; t < g->gtask[j * ngs + gi + 1]; ++t) {
+              const uint32_t c = tp[t + 1] - tp[t];
+              ++hist8[std::min(c / 128u, 8u)];
+              ++nt;
+              np += c;
+              passes += (c + 255u) / 256u;
+            }
+        fprintf(stderr, "[piece stats] %s tasks %llu pieces/task %.1f staging passes/task %.2f | "
+                "by 128-piece bucket:", kind ? "L2" : "LDS", nt, nt ? double(np) / nt : 0.0,
+                nt ? double(passes) / nt : 0.0);
+        for (int q = 0; q < 9; ++q) fprintf(stderr, " %llu", hist8[q]);
+        fprintf(stderr, "\n");
+      }
     }
     // fill the empty runs: T[NB][k] = end of stream k, T[b][k] = T[b+1][k] where empty
     std::vector<uint32_t> hT(tn), hs(RBk.NS);
@@ -2236,7 +2344,18 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
     else hipLaunchKernelGGL((spmv_stream<2, true, false, 5>), gr, bl, lds, s, A);
     return;
   }
+  // PR_LEAN=0: the earlier instruction stream (A/B switch; both give identical sums)
+  const bool lean = g->tune.lean != 0;
+  static bool lattr = false;
+  if (!lattr) {
+    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, true, 0, true>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    lattr = true;
+  }
   if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
+  else if (split && st && lean) hipLaunchKernelGGL((spmv_stream<2, true, true, 0, true>), gr, bl, lds, s, A);
+  else if (split && lean) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true>), gr, bl, lds, s, A);
   else if (split && st) hipLaunchKernelGGL((spmv_stream<2, true, true>), gr, bl, lds, s, A);
   else if (split) hipLaunchKernelGGL((spmv_stream<2, true, false>), gr, bl, lds, s, A);
   else if (st) hipLaunchKernelGGL((spmv_stream<2, false, true>), gr, bl, lds, s, A);

@@ -192,6 +192,27 @@ def test_deterministic_bits(P):
     assert np.array_equal(r1.view(np.uint64), r2.view(np.uint64))
 
 
+@pytest.mark.parametrize("tiny", [False, True])
+def test_lean_stream_bit_identical(P, O, monkeypatch, tiny):
+    """The lean stream instruction stream (PR_LEAN=1: fma-form piece sums, DPP-masked scans,
+    SDWA LDS addresses) computes the same sums in the same order as the earlier form: ranks
+    bit-identical."""
+    if tiny:   # every stream path: several LDS blocks, L2 waves, split segments
+        for k, v in (("PR_HOTLDS", "256"), ("PR_NLDS", "6"), ("PR_QH", "1024"), ("PR_SEG", "512")):
+            monkeypatch.setenv(k, v)
+    out = []
+    for lean in ("0", "1"):
+        monkeypatch.setenv("PR_LEAN", lean)
+        eng = P.Engine()
+        eng.generate_rmat(16, 16, 31)
+        eng.run(8)
+        out.append(eng.ranks())
+        eng.close()
+    for o in out[1:]:
+        assert np.array_equal(out[0].view(np.uint64), o.view(np.uint64))
+    parity.assert_ranks_close(out[-1], O.Graph.from_rmat(16, 16, 31).run(8)["ranks"])
+
+
 def test_convergence_mode(P, O):
     g = O.Graph.from_rmat(14, 16, 3)
     eng = P.Engine()
