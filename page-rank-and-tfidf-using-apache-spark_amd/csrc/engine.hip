@@ -414,7 +414,8 @@ struct StreamArgs {
   uint32_t nlds, H;          // LDS blocks per slice, entries per block
   uint32_t colmask;          // PR_COLMASK (timing experiments only)
   uint32_t dbg;              // PR_DBG timing experiments: 1 no stores, 2 no L2 gathers, 4 no
-                             // starts, 8 no LDS gathers
+                             // starts, 8 no LDS gathers, 2048 / 4096 LDS-group / L2-group
+                             // columns from L2 (wrong sums)
   uint32_t x_bytes;          // bytes of x (< 2^31: the buffer-load range check drops LDS lanes
                              // and PAD_COL padding)
   uint32_t l2mode;           // PR_L2MODE: 0 = L2 tasks interleaved 1/nlds per LDS phase,
@@ -653,7 +654,12 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   const uint32_t l2b = A.gtask[l2g], l2e = A.gtask[l2g + 1];
   const uint64_t l2base = A.gbase[l2g];
   auto fetch = [&](uint32_t tt, bool lds_task, uint32_t gtb, uint64_t gbs) {
-    const uint64_t o = gbs + static_cast<uint64_t>(tt - gtb) * TASK + lane * EPL;
+    // PR_DBG=2048 / 4096 (timing only, wrong sums): every LDS-group / L2-group task reads the
+    // columns of one of its group's first 64 tasks (L2-resident), its own flags and piece base
+    // -- the cost of the column stream's HBM latency (4096 also concentrates the L2 gathers)
+    const bool fake = lds_task ? (A.dbg & 2048u) != 0u : (A.dbg & 4096u) != 0u;
+    const uint32_t tc = fake ? (tt - gtb) % 64u : tt - gtb;
+    const uint64_t o = gbs + static_cast<uint64_t>(tc) * TASK + lane * EPL;
     // groups are padded to whole tasks: these loads never leave the stream buffers
     if (lds_task) {
       const u32x4* cp = reinterpret_cast<const u32x4*>(col16 + o);
@@ -855,7 +861,21 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (!(A.dbg & 1u))
+      if (LEAN && !(A.dbg & 1u)) {
+        // two pieces per lane per store instruction (16 B at 8-B alignment: the device runs
+        // in unaligned mode), half the store instructions (+0.8 %, profiles/r02/vmem); a
+        // trailing odd piece goes alone
+        typedef double d2v __attribute__((ext_vector_type(2)));
+#pragma unroll 1
+        for (uint32_t i = 2u * static_cast<uint32_t>(lane); i < wn; i += 128u) {
+          if (i + 1u < wn) {
+            const d2v pr = *reinterpret_cast<const d2v*>(stg + i);
+            __builtin_nontemporal_store(pr, reinterpret_cast<d2v*>(part + tp0 + w0 + i));
+          } else {
+            __builtin_nontemporal_store(stg[i], part + tp0 + w0 + i);
+          }
+        }
+      } else if (!(A.dbg & 1u))
         for (uint32_t i = lane; i < wn; i += 64) {
           if constexpr (NT >= 2) __builtin_nontemporal_store(stg[i], part + tp0 + w0 + i);
           else part[tp0 + w0 + i] = stg[i];
