@@ -136,7 +136,7 @@ int build_device(pr_ctx* c, const prmi::BuildInput& in0) {
             c->opts.rank, U(2ull * g.n_col16), U(4ull * g.n_col32), U(g.stream_len / 8),
             U(4ull * (g.ntask + 1ull)), U(std::min<uint64_t>(xlds, 8ull * g.X)),
             U(8ull * g.X - std::min<uint64_t>(xlds, 8ull * g.X)), U(8ull * g.n_pieces),
-            U(8ull * g.n_pieces), U(2ull * 64 * 8 * g.n_groups),
+            U(8ull * g.n_pieces), U(12ull * 64 * g.n_groups),
             U(12ull * g.n_lines + 4ull * g.n_runs + 12ull * g.nb_rows), U(4ull * g.lrows),
             U(8ull * g.lA), U(g.n_col16), U(g.n_col32), U(g.n_lines), U(g.n_runs));
   }

@@ -150,7 +150,8 @@ struct DevGraph {
   uint32_t* lfirst = nullptr;     // [lines] block-relative run of the line's first piece
   uint64_t* lmask = nullptr;      // [lines] run starts inside the line
   uint32_t* goff = nullptr;       // [nb_rows + 1] first 8-line group of each block
-  uint16_t* roffL = nullptr;      // [groups * 64 * 8] row offsets in row-launch order
+  uint32_t* roffL = nullptr;      // [groups * 64 * 3] row offsets in row-launch order (10-bit, 3 per dword)
+  bool roff16 = false;            // PR_ROFF16: the earlier 8 x u16 layout (A/B only)
   uint32_t* meta = nullptr;
   uint32_t* perm = nullptr;       // internal -> original
   uint32_t* outdeg = nullptr;     // by original id

@@ -181,8 +181,11 @@ struct RowArgs {
   const uint32_t* lfirst;  // [lines + pad] run (block-relative) of each line's first piece
   const uint64_t* lmask;   // [lines + pad] bit j: piece j of the line starts a run (j >= 1)
   const double* partial;   // per-piece partial sums of this round
-  const uint16_t* roffL;   // row offsets in row-launch order: per 8-line group, lane-major
-                           // (lane l's 8 values in one 16-byte word)
+  const uint32_t* roffL;   // row offsets in row-launch order: per 8-line group, lane-major,
+                           // lane l's 8 ten-bit values packed 3 per dword (12 bytes: value u
+                           // in dword u / 3 at bit 10 (u % 3); RB = 1024 rows need 10 bits)
+  uint32_t roffL_bytes;    // bytes of roffL (the buffer-load range)
+  uint32_t roff16;         // PR_ROFF16=1: the earlier layout (8 x u16 per lane per group, A/B)
   const uint32_t* goff;    // [NB + 1] first 8-line group of each block
   uint32_t NS, nbA, lA, lrows;
   uint32_t rb;             // rows per block (<= RB)
@@ -336,7 +339,9 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
       ma[u] = lm[Lb + u];
     }
   };
-  typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+  typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+  const __amdgpu_buffer_rsrc_t rofr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(A.roffL), static_cast<short>(0), static_cast<int>(A.roffL_bytes), 0x00020000);
   auto issue = [&](uint32_t L, double (&vv)[EPR], uint32_t (&rr)[EPR]) {
 #pragma unroll
     for (int u = 0; u < EPR; ++u) {
@@ -346,10 +351,21 @@ __global__ __launch_bounds__(BLOCK) void spmv_rows(RowArgs A) {
       if (A.dbg & 128u) vv[u] = __builtin_nontemporal_load(A.partial + pc);  // experiment
       else vv[u] = A.partial[pc];
     }
-    const u16x8 r8 = *reinterpret_cast<const u16x8*>(
-        A.roffL + ((static_cast<uint64_t>(G0 + L / EPR) * 64u) + static_cast<uint32_t>(lane)) * EPR);
+    // one 12-byte load per step: lane l's 8 row offsets, 10 bits each (buffer offsets are
+    // 32-bit: roffL stays below 4 GiB, 768 bytes per 8-line group)
+    if (A.roff16) {
+      typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+      const u16x8 r8 = *reinterpret_cast<const u16x8*>(
+          reinterpret_cast<const uint16_t*>(A.roffL) +
+          ((static_cast<uint64_t>(G0 + L / EPR) * 64u) + static_cast<uint32_t>(lane)) * EPR);
 #pragma unroll
-    for (int u = 0; u < EPR; ++u) rr[u] = r8[u];
+      for (int u = 0; u < EPR; ++u) rr[u] = r8[u];
+    } else {
+      const u32x3 r3 = __builtin_amdgcn_raw_buffer_load_b96(
+          rofr, ((G0 + L / EPR) * 64u + static_cast<uint32_t>(lane)) * 12u, 0, 0);
+#pragma unroll
+      for (int u = 0; u < EPR; ++u) rr[u] = (r3[u / 3] >> (10 * (u % 3))) & 0x3FFu;
+    }
     maps(L + EPR);
   };
   auto add = [&](uint32_t L, const double (&vv)[EPR], const uint32_t (&rr)[EPR]) {
@@ -1396,21 +1412,32 @@ __global__ __launch_bounds__(BLOCK) void k_roff_lines(const uint16_t* roff, cons
                                                       const uint32_t* ne_off, const uint32_t* l_off,
                                                       const uint32_t* btot, const uint32_t* lfirst,
                                                       const uint64_t* lmask, const uint32_t* goff,
-                                                      uint16_t* roffL) {
+                                                      uint32_t* roffL, uint32_t roff16) {
   const uint32_t b = blockIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t L0 = l_off[b], nl = l_off[b + 1] - L0, tot = btot[b], ne0 = ne_off[b];
   const uint32_t G0 = goff[b], ng = (nl + EPR - 1) / EPR;
   const uint64_t lbits = (2ull << lane) - 2ull;
   for (uint32_t gi = wv; gi < ng; gi += BLOCK / 64) {
+    uint32_t w[3] = {0u, 0u, 0u};
     for (int u = 0; u < EPR; ++u) {
       const uint32_t L = gi * EPR + u, i = L * 64u + static_cast<uint32_t>(lane);
-      uint16_t r = 0;
+      uint32_t r = 0;
       if (L < nl && i < tot) {
         const uint32_t q = lfirst[L0 + L] + static_cast<uint32_t>(__popcll(lmask[L0 + L] & lbits));
-        r = roff[nebase[ne0 + q] + i];
+        r = roff[nebase[ne0 + q] + i];  // < RB = 1024: 10 bits
       }
-      roffL[((static_cast<uint64_t>(G0 + gi) * 64u) + static_cast<uint32_t>(lane)) * EPR + u] = r;
+      w[u / 3] |= r << (10 * (u % 3));
+    }
+    const uint64_t gl = (static_cast<uint64_t>(G0 + gi) * 64u) + static_cast<uint32_t>(lane);
+    if (roff16) {  // the earlier layout: lane l's 8 offsets as 8 x u16 in 16 bytes
+      uint16_t* d16 = reinterpret_cast<uint16_t*>(roffL) + gl * EPR;
+      for (int u = 0; u < EPR; ++u) d16[u] = static_cast<uint16_t>((w[u / 3] >> (10 * (u % 3))) & 0x3FFu);
+    } else {
+      uint32_t* dst = roffL + gl * 3u;
+      dst[0] = w[0];
+      dst[1] = w[1];
+      dst[2] = w[2];
     }
   }
 }
@@ -2273,9 +2300,16 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
       hgoff[NB] = static_cast<uint32_t>(groups);
       g->n_groups = groups;
       TRY(dmalloc(&g->goff, NB + 1ull, err));
-      TRY(dmalloc(&g->roffL, std::max<uint64_t>(groups, 1) * 64 * EPR, err));
+      // 12 bytes per (group, lane); the row launch reads it through a buffer resource with
+      // 32-bit offsets
+      if (std::max<uint64_t>(groups, 1) * 64 * 12 >= (1ull << 32)) {
+        if (err) *err = "row-launch groups exceed the 4 GiB row-offset buffer";
+        return PR_E_ARG;
+      }
+      g->roff16 = env_int("PR_ROFF16", 0) != 0;
+      TRY(dmalloc(&g->roffL, std::max<uint64_t>(groups, 1) * 64 * (g->roff16 ? 4 : 3), err));
       HIPTRY(hipMemcpyAsync(g->goff, hgoff.data(), 4ull * (NB + 1), hipMemcpyHostToDevice, s));
-      if (NB) hipLaunchKernelGGL(k_roff_lines, dim3(NB), dim3(BLOCK), 0, s, g->roff, g->nebase, g->ne_off, g->l_off, g->btot, g->lfirst, g->lmask, g->goff, g->roffL);
+      if (NB) hipLaunchKernelGGL(k_roff_lines, dim3(NB), dim3(BLOCK), 0, s, g->roff, g->nebase, g->ne_off, g->l_off, g->btot, g->lfirst, g->lmask, g->goff, g->roffL, g->roff16 ? 1u : 0u);
       HIPTRY(hipGetLastError());
       HIPTRY(hipStreamSynchronize(s));
     }
@@ -2492,6 +2526,8 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
   A.lmask = g->lmask;
   A.partial = g->partial;
   A.roffL = g->roffL;
+  A.roffL_bytes = static_cast<uint32_t>(std::max<uint64_t>(g->n_groups, 1) * 64 * 12);
+  A.roff16 = g->roff16 ? 1u : 0u;
   A.goff = g->goff;
   A.dbg = static_cast<uint32_t>(g->tune.dbg);
   A.NS = g->n_streams;

@@ -213,6 +213,31 @@ def test_lean_stream_bit_identical(P, O, monkeypatch, tiny):
     parity.assert_ranks_close(out[-1], O.Graph.from_rmat(16, 16, 31).run(8)["ranks"])
 
 
+@pytest.mark.parametrize("p", [1, 3])
+def test_row_offset_layouts_bit_identical(P, O, monkeypatch, p):
+    """The 10-bit packed row offsets of the row launch (3 per dword, one 12-byte load per
+    step) and the earlier 8 x u16 layout (PR_ROFF16=1) feed the same adds: ranks
+    bit-identical, with heavy blocks and at several ranks."""
+    monkeypatch.setenv("PR_HDEG", "40")
+    out = []
+    for lay in ("1", "0"):
+        monkeypatch.setenv("PR_ROFF16", lay)
+        if p == 1:
+            eng = P.Engine()
+            eng.generate_rmat(17, 16, 35)
+            eng.run(6)
+            out.append(eng.ranks())
+            eng.close()
+        else:
+            grp = P.LocalGroup(p)
+            grp.each("generate_rmat", 17, 16, 35)
+            grp.run(6)
+            out.append(grp.members[0].ranks())
+            grp.close()
+    assert np.array_equal(out[0].view(np.uint64), out[1].view(np.uint64))
+    parity.assert_ranks_close(out[1], O.Graph.from_rmat(17, 16, 35).run(6)["ranks"])
+
+
 def test_convergence_mode(P, O):
     g = O.Graph.from_rmat(14, 16, 3)
     eng = P.Engine()
