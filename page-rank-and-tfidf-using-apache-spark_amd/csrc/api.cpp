@@ -51,6 +51,8 @@ struct pr_ctx {
   std::vector<hipEvent_t> ev_chunk;
   hipEvent_t ev_rec = nullptr, ev_done = nullptr;
   int xchunks = 4;                // PR_XCHUNKS: row-launch chunks of the x' exchange
+  int sx_checked = 0;             // sparse exchange: chunk count whose lists the ranks agreed on
+  bool sx_ok = false;             //   (RCCL: count matrices compared once, all ranks alike)
   bool ingest_fallback = false;  // last text ingest went to the host parser (too large)
   // caller-staged exchange (pr_comm_init_external / pr_ext_*): the caller moves each
   // round's x slot + exact record between ranks with a transport of its own
@@ -101,6 +103,63 @@ int need_comm(pr_ctx* c) {
   return PR_OK;
 }
 
+// Sparse x' exchange (PR_SPARSE_X: -1 = from 4 ranks on, 0 = off, 1 = on): only the x'
+// entries a peer's edges reference travel (at p = 8 about 55 % of a slot).
+bool want_sx(const pr_ctx* c) {
+  int v = -1;
+  if (const char* e = getenv("PR_SPARSE_X")) v = atoi(e);
+  return c->opts.n_ranks > 1 && (v > 0 || (v < 0 && c->opts.n_ranks >= 4));
+}
+
+// RCCL ranks: build the lists, then check once that every rank's receive counts equal its
+// peers' send counts (an all-gather of the count matrices); any mismatch anywhere turns the
+// sparse exchange off on every rank (a count mismatch inside a grouped send/recv would hang)
+int sx_setup_rccl(pr_ctx* c, const std::vector<prmi::XChunk>& plan, bool& sx) {
+  DevGraph* g = &c->dg;
+  const int p = c->opts.n_ranks, K = static_cast<int>(plan.size());
+  if (c->sx_checked == K) {
+    sx = c->sx_ok;
+    return PR_OK;
+  }
+  // a rank whose lists fail to build still joins the two collectives below (with a veto), so
+  // no rank waits alone; every rank then runs the dense exchange
+  std::string e;
+  const int prep = prmi::dev_sx_prepare(g, plan, &e);
+  const size_t m = static_cast<size_t>(K) * p;
+  std::vector<uint64_t> mine(m, 0), all(m * p, 0);
+  if (!prep)
+    for (size_t i = 0; i < m; ++i) mine[i] = g->sx_so[i + 1] - g->sx_so[i];
+  if (prep) fprintf(stderr, "[prmi355x] rank %d: sparse exchange lists: %s\n", c->opts.rank, e.c_str());
+  uint64_t *d_cnt = nullptr, *d_flag = nullptr;
+  HIPCHK(c, hipMalloc(&d_cnt, 8 * (m + m * p)));
+  HIPCHK(c, hipMalloc(&d_flag, 8));
+  HIPCHK(c, hipMemcpy(d_cnt, mine.data(), 8 * m, hipMemcpyHostToDevice));
+  ncclResult_t nr = ncclAllGather(d_cnt, d_cnt + m, m, ncclUint64, c->comm, c->stream);
+  if (nr == ncclSuccess && hipStreamSynchronize(c->stream) == hipSuccess)
+    (void)hipMemcpy(all.data(), d_cnt + m, 8 * m * p, hipMemcpyDeviceToHost);
+  uint64_t bad = (nr == ncclSuccess && !prep) ? 0 : 1;
+  for (int k = 0; k < K && !bad; ++k)
+    for (int r = 0; r < p; ++r) {
+      if (r == c->opts.rank) continue;
+      const size_t me = static_cast<size_t>(k) * p + c->opts.rank, i = static_cast<size_t>(k) * p + r;
+      if (all[static_cast<size_t>(r) * m + me] != g->sx_ro[i + 1] - g->sx_ro[i]) bad = 1;
+    }
+  if (nr == ncclSuccess) {
+    (void)hipMemcpy(d_flag, &bad, 8, hipMemcpyHostToDevice);
+    nr = ncclAllReduce(d_flag, d_flag, 1, ncclUint64, ncclSum, c->comm, c->stream);
+    if (nr == ncclSuccess && hipStreamSynchronize(c->stream) == hipSuccess)
+      (void)hipMemcpy(&bad, d_flag, 8, hipMemcpyDeviceToHost);
+  }
+  (void)hipFree(d_cnt);
+  (void)hipFree(d_flag);
+  if (nr != ncclSuccess) return fail(c, PR_E_RCCL, std::string("sparse exchange check: ") + ncclGetErrorString(nr));
+  if (bad) fprintf(stderr, "[prmi355x] rank %d: sparse exchange lists disagree across ranks; dense exchange\n", c->opts.rank);
+  c->sx_checked = K;
+  c->sx_ok = bad == 0;
+  sx = c->sx_ok;
+  return PR_OK;
+}
+
 // comm stream + events of the chunked exchange (created on first use)
 int ensure_xchg(pr_ctx* c) {
   if (!c->comm_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
@@ -115,6 +174,7 @@ int build_device(pr_ctx* c, const prmi::BuildInput& in0) {
   prmi::BuildInput in = in0;
   in.normalized = (c->opts.flags & PR_F_NORMALIZED) != 0;
   c->seed_rounds = 0;
+  c->sx_checked = 0;  // a new graph: the sparse-exchange lists are rebuilt and re-checked
   int rc = prmi::dev_build(&c->dg, in, c->stream, &e);
   if (rc) return fail(c, rc, "device build: " + e);
   c->last_iters = -1;
@@ -558,6 +618,26 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
   }
   for (int i = 1; i < n; ++i)
     if (plans[i].size() != plans[0].size()) return fail(c0, PR_E_ARG, "local group: exchange plans differ");
+  // sparse exchange: every member's lists, and rank r's send counts to q equal q's receive
+  // counts from r for every chunk (the lists of pr_run's RCCL path, checked here on the host)
+  const bool sx = n > 1 && want_sx(c0);
+  if (sx) {
+    for (int i = 0; i < n; ++i) {
+      HIPCHK(c0, hipSetDevice(ctxs[i]->device));
+      std::string e;
+      int rc = prmi::dev_sx_prepare(&ctxs[i]->dg, plans[i], &e);
+      if (rc) return fail(c0, rc, "sparse exchange: " + e);
+    }
+    for (size_t k = 0; k < plans[0].size(); ++k)
+      for (int r = 0; r < n; ++r)
+        for (int q = 0; q < n; ++q) {
+          if (q == r) continue;
+          const size_t is = k * n + q, ir = k * n + r;
+          const DevGraph &gr = ctxs[r]->dg, &gq = ctxs[q]->dg;
+          if (gr.sx_so[is + 1] - gr.sx_so[is] != gq.sx_ro[ir + 1] - gq.sx_ro[ir])
+            return fail(c0, PR_E_ARG, "sparse exchange: send / receive lists disagree");
+        }
+  }
   for (int t = 1; t <= iterations; ++t) {
     const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
     prmi::Span round("prmi:round");
@@ -570,6 +650,7 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       int rc = prmi::dev_round_stream(&m->dg, t, m->stream, nullptr);
       for (size_t k = 0; !rc && k < plans[i].size(); ++k) {
         rc = prmi::dev_round_rows(&m->dg, t, mode, plans[i][k].b0, plans[i][k].b1, m->stream);
+        if (!rc && sx) rc = prmi::dev_sx_pack(&m->dg, t, static_cast<int>(k), m->stream);
         if (!rc && hipEventRecord(m->ev_chunk[k], m->stream) != hipSuccess) rc = PR_E_HIP;
       }
       if (!rc) rc = prmi::dev_round_rows(&m->dg, t, mode, m->dg.nb_rows_a, m->dg.nb_rows, m->stream);
@@ -581,17 +662,31 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       pr_ctx* mq = ctxs[q];
       DevGraph* dst = &mq->dg;
       HIPCHK(c0, hipSetDevice(mq->device));
-      for (size_t k = 0; k < plans[q].size(); ++k)
+      for (size_t k = 0; k < plans[q].size(); ++k) {
         for (int r = 0; r < n; ++r) {
           if (r == q) continue;
           DevGraph* src = &ctxs[r]->dg;
           HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ctxs[r]->ev_chunk[k], 0));
+          if (sx) {  // r's packed entries for q -> q's receive buffer, as ncclSend / ncclRecv
+            const size_t is = k * n + q, ir = k * n + r;
+            const uint64_t cnt = src->sx_so[is + 1] - src->sx_so[is];
+            if (cnt)
+              HIPCHK(c0, hipMemcpyPeerAsync(dst->sx_rbuf + dst->sx_ro[ir], mq->device,
+                                            src->sx_sbuf + src->sx_so[is], ctxs[r]->device,
+                                            8ull * cnt, mq->comm_stream));
+            continue;
+          }
           const uint64_t base = static_cast<uint64_t>(r) * src->maxA;
           for (const prmi::XPiece& pc : plans[q][k].pieces)
             HIPCHK(c0, hipMemcpyPeerAsync(prmi::dev_x_out(dst, t) + base + pc.off, mq->device,
                                           prmi::dev_x_out(src, t) + base + pc.off, ctxs[r]->device,
                                           8ull * pc.cnt, mq->comm_stream));
         }
+        if (sx) {
+          int rc = prmi::dev_sx_unpack(dst, t, static_cast<int>(k), mq->comm_stream);
+          if (rc) return fail(c0, rc, "sparse exchange unpack");
+        }
+      }
       for (int r = 0; r < n; ++r) {
         DevGraph* src = &ctxs[r]->dg;
         HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ctxs[r]->ev_rec, 0));
@@ -933,6 +1028,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   prmi::IterState hs{};
   const int p = c->opts.n_ranks;
   std::vector<prmi::XChunk> plan;
+  bool sx = false;  // sparse x' exchange this run
   if (p > 1) {
     rc = ensure_xchg(c);
     if (rc) return rc;
@@ -941,6 +1037,10 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       hipEvent_t e;
       HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
       c->ev_chunk.push_back(e);
+    }
+    if (want_sx(c)) {
+      rc = sx_setup_rccl(c, plan, sx);
+      if (rc) return rc;
     }
   }
   for (int t = 1; t <= iterations; ++t) {
@@ -965,6 +1065,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       if (rc) return fail(c, rc, "round compute");
       for (size_t k = 0; k < plan.size(); ++k) {
         rc = prmi::dev_round_rows(g, t, mode, plan[k].b0, plan[k].b1, c->stream);
+        if (!rc && sx) rc = prmi::dev_sx_pack(g, t, static_cast<int>(k), c->stream);
         if (rc) return fail(c, rc, "round rows");
         HIPCHK(c, hipEventRecord(c->ev_chunk[k], c->stream));
       }
@@ -975,13 +1076,27 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       for (size_t k = 0; k < plan.size(); ++k) {
         HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_chunk[k], 0));
         NCCLCHK(c, ncclGroupStart());
-        for (const prmi::XPiece& pc : plan[k].pieces)
+        if (sx) {  // the packed entries each peer references (counts agreed in sx_setup_rccl)
           for (int q = 0; q < p; ++q) {
             if (q == g->rank) continue;
-            NCCLCHK(c, ncclSend(xf + static_cast<uint64_t>(g->rank) * g->maxA + pc.off, pc.cnt, ncclFloat64, q, c->comm, c->comm_stream));
-            NCCLCHK(c, ncclRecv(xf + static_cast<uint64_t>(q) * g->maxA + pc.off, pc.cnt, ncclFloat64, q, c->comm, c->comm_stream));
+            const size_t i = k * p + q;
+            const uint64_t ns = g->sx_so[i + 1] - g->sx_so[i], nrv = g->sx_ro[i + 1] - g->sx_ro[i];
+            if (ns) NCCLCHK(c, ncclSend(g->sx_sbuf + g->sx_so[i], ns, ncclFloat64, q, c->comm, c->comm_stream));
+            if (nrv) NCCLCHK(c, ncclRecv(g->sx_rbuf + g->sx_ro[i], nrv, ncclFloat64, q, c->comm, c->comm_stream));
           }
+        } else {
+          for (const prmi::XPiece& pc : plan[k].pieces)
+            for (int q = 0; q < p; ++q) {
+              if (q == g->rank) continue;
+              NCCLCHK(c, ncclSend(xf + static_cast<uint64_t>(g->rank) * g->maxA + pc.off, pc.cnt, ncclFloat64, q, c->comm, c->comm_stream));
+              NCCLCHK(c, ncclRecv(xf + static_cast<uint64_t>(q) * g->maxA + pc.off, pc.cnt, ncclFloat64, q, c->comm, c->comm_stream));
+            }
+        }
         NCCLCHK(c, ncclGroupEnd());
+        if (sx) {
+          rc = prmi::dev_sx_unpack(g, t, static_cast<int>(k), c->comm_stream);
+          if (rc) return fail(c, rc, "sparse exchange unpack");
+        }
       }
       HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_rec, 0));
       NCCLCHK(c, ncclAllGather(g->rec_local, g->rec_all, prmi::REC_WORDS, ncclUint64, c->comm, c->comm_stream));

@@ -173,6 +173,18 @@ struct DevGraph {
   uint64_t* shards = nullptr;     // [NSHARD][REC_WORDS]
   uint64_t* rec_local = nullptr;  // [REC_WORDS]
   uint64_t* rec_all = nullptr;    // [p][REC_WORDS]
+  // sparse x' exchange (p > 1): which class-A x entries each rank's edges reference, computed
+  // at build from the replicated edge set (no exchange needed to agree on it).  sx_send bit
+  // q * maxA + o: peer q references entry o of this rank's slot; sx_recv bit x: this rank
+  // references x position x of a peer's slot.  Host copies; the per-chunk lists are built at
+  // the first exchanged run (dev_sx_prepare).
+  std::vector<uint32_t> sx_send, sx_recv;
+  uint32_t* sx_spos = nullptr;    // [sends] slot-relative entries to pack, by (chunk, peer)
+  uint32_t* sx_rpos = nullptr;    // [recvs] absolute x positions to unpack, by (chunk, peer)
+  double* sx_sbuf = nullptr;      // [sends]
+  double* sx_rbuf = nullptr;      // [recvs]
+  std::vector<uint64_t> sx_so, sx_ro;  // [chunks * p + 1] offsets of each (chunk, peer) list
+  int sx_chunks = 0;              // chunk count the lists were built for (0 = none)
   IterState* state = nullptr;
   // row launch: blocks of 1024 rows (class A, then class B), streams = slices x segments
   uint32_t nb_rows = 0, nb_rows_a = 0, n_streams = 0;
@@ -219,6 +231,13 @@ struct XChunk {
   std::vector<XPiece> pieces;
 };
 std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K);
+// Sparse exchange: build the per-(chunk, peer) pack / unpack lists for `plan` (once per chunk
+// count); pack chunk k of this rank's slot of x'(t) into sx_sbuf; unpack chunk k's received
+// entries from sx_rbuf into x'(t).  Lists are in (chunk, peer, piece, entry) order on every
+// rank, so rank r's send list for q is q's receive list for r.
+int dev_sx_prepare(DevGraph* g, const std::vector<XChunk>& plan, std::string* err);
+int dev_sx_pack(DevGraph* g, int t, int k, hipStream_t s);
+int dev_sx_unpack(DevGraph* g, int t, int k, hipStream_t s);
 // After the exchange: combine p records -> next round's addthis / error / residual.
 int dev_round_finalize(DevGraph* g, int t, bool tracked, hipStream_t s);
 // Round-1 state (r^0 == 1): a = W0 / n_tot.

@@ -1283,6 +1283,36 @@ __global__ void k_stream_keys(const uint64_t* uk, uint64_t nnz, int nb, const ui
   }
 }
 
+// sparse x' exchange: mark the class-A x entries that cross ranks.  Edge (dst kd, src ks):
+// the row's owner q reads source ks, whose x' lives in owner r's slot.  A plain load first, so
+// hub sources (one word, many edges) cost one atomic per word, not one per edge.
+__global__ void k_sx_bits(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv, Layout L,
+                          uint32_t* sbits, uint32_t* rbits) {
+  PRMI_BLOCK_LOOP(nnz) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    if (e >= nnz) continue;
+    const uint64_t k = uk[e];
+    const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
+    const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
+    if (ks >= L.nA) continue;  // class-C sources are constant after round 1: never exchanged
+    const uint32_t q = owner_of(L, kd), r = owner_of(L, ks);
+    if (q == r || (q != L.rank && r != L.rank)) continue;
+    const uint32_t xp = xpos(L, ks);  // inside slot r
+    const uint64_t bit = r == L.rank ? static_cast<uint64_t>(q) * L.maxA + (xp - r * L.maxA) : xp;
+    uint32_t* w = (r == L.rank ? sbits : rbits) + (bit >> 5);
+    const uint32_t m = 1u << (bit & 31);
+    if (!(__builtin_nontemporal_load(w) & m)) atomicOr(w, m);
+  }
+}
+__global__ void k_sx_pack(const double* slot, const uint32_t* pos, uint64_t n, double* buf) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) buf[i] = slot[pos[i]];
+}
+__global__ void k_sx_unpack(double* x, const uint32_t* pos, uint64_t n, const double* buf) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) x[pos[i]] = buf[i];
+}
+
 // first sorted edge of each stream group (atomicMin; empty groups keep the sentinel)
 __global__ void k_group_starts(const uint64_t* key, uint64_t n, StreamGeo G,
                                unsigned long long* starts) {
@@ -1715,6 +1745,7 @@ void dev_free(DevGraph* g) {
   F(g->col); F(g->bits); F(g->task_piece); F(g->partial); F(g->roff); F(g->runs);
   F(g->nebase); F(g->ne_off); F(g->l_off); F(g->btot); F(g->lfirst); F(g->lmask);
   F(g->goff); F(g->roffL);
+  F(g->sx_spos); F(g->sx_rpos); F(g->sx_sbuf); F(g->sx_rbuf);
   F(g->d_gtask); F(g->d_gstart); F(g->d_gbase); F(g->col16);
   F(g->meta); F(g->perm); F(g->outdeg); F(g->indeg); F(g->dang_w);
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
@@ -2010,6 +2041,22 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   HIPTRY(hipMemsetAsync(d_cnt, 0, 16, s));
   HIPTRY(hipMemsetAsync(d_cnt + 2, 0xFF, 8ull * NG, s));
   if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, lk_in);
+  if (p > 1 && g->maxA) {  // sparse x' exchange: the cross-rank entries (host bitmaps)
+    const uint64_t words = (static_cast<uint64_t>(p) * g->maxA + 31) / 32;
+    uint32_t *sb = nullptr, *rb = nullptr;
+    TRY(dmalloc(&sb, words, err));
+    TRY(dmalloc(&rb, words, err));
+    HIPTRY(hipMemsetAsync(sb, 0, 4 * words, s));
+    HIPTRY(hipMemsetAsync(rb, 0, 4 * words, s));
+    if (nnz) hipLaunchKernelGGL(k_sx_bits, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, sb, rb);
+    g->sx_send.resize(words);
+    g->sx_recv.resize(words);
+    HIPTRY(hipMemcpyAsync(g->sx_send.data(), sb, 4 * words, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipMemcpyAsync(g->sx_recv.data(), rb, 4 * words, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(sb);
+    (void)hipFree(rb);
+  }
   uint64_t lnnz = nnz;
   uint64_t* lk_alt = uniq;  // the unique keys are dead from here: sort scratch
   if (p > 1 && nnz) {  // keep this rank's rows' edges (order-preserving select)
@@ -2614,6 +2661,77 @@ std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K) {
     bprev = b1;
   }
   return out;
+}
+
+int dev_sx_prepare(DevGraph* g, const std::vector<XChunk>& plan, std::string* err) {
+  const uint32_t p = static_cast<uint32_t>(g->p), me = static_cast<uint32_t>(g->rank);
+  const int K = static_cast<int>(plan.size());
+  if (g->sx_chunks == K) return PR_OK;
+  if (p < 2 || g->sx_send.empty()) {
+    if (err) *err = "sparse exchange: no cross-rank bitmaps (single rank?)";
+    return PR_E_ARG;
+  }
+  for (void* q : {static_cast<void*>(g->sx_spos), static_cast<void*>(g->sx_rpos),
+                  static_cast<void*>(g->sx_sbuf), static_cast<void*>(g->sx_rbuf)})
+    if (q) (void)hipFree(q);
+  g->sx_spos = g->sx_rpos = nullptr;
+  g->sx_sbuf = g->sx_rbuf = nullptr;
+  auto bit = [](const std::vector<uint32_t>& b, uint64_t i) { return (b[i >> 5] >> (i & 31)) & 1u; };
+  std::vector<uint32_t> sp, rp;
+  g->sx_so.assign(static_cast<size_t>(K) * p + 1, 0);
+  g->sx_ro.assign(static_cast<size_t>(K) * p + 1, 0);
+  for (int k = 0; k < K; ++k)
+    for (uint32_t q = 0; q < p; ++q) {
+      g->sx_so[static_cast<size_t>(k) * p + q] = sp.size();
+      g->sx_ro[static_cast<size_t>(k) * p + q] = rp.size();
+      if (q == me) continue;
+      for (const XPiece& pc : plan[k].pieces)
+        for (uint64_t o = pc.off; o < pc.off + pc.cnt && o < g->maxA; ++o) {
+          if (bit(g->sx_send, static_cast<uint64_t>(q) * g->maxA + o)) sp.push_back(static_cast<uint32_t>(o));
+          const uint64_t xq = static_cast<uint64_t>(q) * g->maxA + o;
+          if (bit(g->sx_recv, xq)) rp.push_back(static_cast<uint32_t>(xq));
+        }
+    }
+  g->sx_so.back() = sp.size();
+  g->sx_ro.back() = rp.size();
+  if (getenv("PR_VERBOSE"))
+    fprintf(stderr, "[prmi355x] rank %u sparse x' exchange: sends %zu entries, receives %zu (dense: %llu each way, %.1f %% / %.1f %%)\n",
+            me, sp.size(), rp.size(), static_cast<unsigned long long>(p - 1) * g->maxA,
+            100.0 * sp.size() / std::max<double>(1.0, static_cast<double>(p - 1) * g->maxA),
+            100.0 * rp.size() / std::max<double>(1.0, static_cast<double>(p - 1) * g->maxA));
+  if (!sp.empty()) {
+    TRY(dmalloc(&g->sx_spos, sp.size(), err));
+    TRY(dmalloc(&g->sx_sbuf, sp.size(), err));
+    HIPTRY(hipMemcpy(g->sx_spos, sp.data(), 4 * sp.size(), hipMemcpyHostToDevice));
+  }
+  if (!rp.empty()) {
+    TRY(dmalloc(&g->sx_rpos, rp.size(), err));
+    TRY(dmalloc(&g->sx_rbuf, rp.size(), err));
+    HIPTRY(hipMemcpy(g->sx_rpos, rp.data(), 4 * rp.size(), hipMemcpyHostToDevice));
+  }
+  g->sx_chunks = K;
+  return PR_OK;
+}
+
+int dev_sx_pack(DevGraph* g, int t, int k, hipStream_t s) {
+  std::string* err = nullptr;
+  const uint64_t a = g->sx_so[static_cast<size_t>(k) * g->p], b = g->sx_so[static_cast<size_t>(k + 1) * g->p];
+  if (b > a)
+    hipLaunchKernelGGL(k_sx_pack, dim3(static_cast<uint32_t>((b - a + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                       dev_x_out(g, t) + static_cast<uint64_t>(g->rank) * g->maxA, g->sx_spos + a, b - a,
+                       g->sx_sbuf + a);
+  HIPTRY(hipGetLastError());
+  return PR_OK;
+}
+
+int dev_sx_unpack(DevGraph* g, int t, int k, hipStream_t s) {
+  std::string* err = nullptr;
+  const uint64_t a = g->sx_ro[static_cast<size_t>(k) * g->p], b = g->sx_ro[static_cast<size_t>(k + 1) * g->p];
+  if (b > a)
+    hipLaunchKernelGGL(k_sx_unpack, dim3(static_cast<uint32_t>((b - a + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                       dev_x_out(g, t), g->sx_rpos + a, b - a, g->sx_rbuf + a);
+  HIPTRY(hipGetLastError());
+  return PR_OK;
 }
 
 int dev_round_finalize(DevGraph* g, int t, bool tracked, hipStream_t s) {

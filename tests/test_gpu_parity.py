@@ -238,6 +238,26 @@ def test_row_offset_layouts_bit_identical(P, O, monkeypatch, p):
     parity.assert_ranks_close(out[1], O.Graph.from_rmat(17, 16, 35).run(6)["ranks"])
 
 
+@pytest.mark.parametrize("p,tiny", [(4, False), (8, False), (2, True), (4, True)])
+def test_sparse_exchange_bit_identical(P, O, monkeypatch, p, tiny):
+    """The sparse x' exchange (PR_SPARSE_X: only the entries a peer's edges reference travel,
+    packed per (chunk, peer)) leaves every rank the same x values to gather: ranks bit-identical
+    to the dense exchange, and the oracle's."""
+    if tiny:
+        for k, v in (("PR_HOTLDS", "256"), ("PR_NLDS", "6"), ("PR_QH", "1024"), ("PR_SEG", "512")):
+            monkeypatch.setenv(k, v)
+    out = []
+    for sx in ("0", "1"):
+        monkeypatch.setenv("PR_SPARSE_X", sx)
+        grp = P.LocalGroup(p)
+        grp.each("generate_rmat", 16, 16, 37)
+        grp.run(9)
+        out.append(grp.members[0].ranks())
+        grp.close()
+    assert np.array_equal(out[0].view(np.uint64), out[1].view(np.uint64))
+    parity.assert_ranks_close(out[1], O.Graph.from_rmat(16, 16, 37).run(9)["ranks"])
+
+
 def test_convergence_mode(P, O):
     g = O.Graph.from_rmat(14, 16, 3)
     eng = P.Engine()
