@@ -161,6 +161,7 @@ def main():
                        "vertices": n, "distinct_edges": nnz, "rounds_per_step": 1,
                        "parallelism": f"rows dealt over {world} GPUs, chunked RCCL p2p "
                                       f"exchange of x' overlapped with the row launch"
+                                      + (" (sparse: referenced entries only)" if world >= 4 else "")
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
