@@ -140,6 +140,8 @@ def main():
     kms = st["ms_spmv_kernel"]
     achieved = bytes_launch / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = load_traffic(a.traffic_json, f"{workload}-p{world}")
+    sx_env = int(os.environ.get("PR_SPARSE_X", "-1"))   # the engine's rule (api.cpp want_sx)
+    sparse_x = world > 1 and (sx_env > 0 or (sx_env < 0 and world >= 4))
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(eng, a.cpu_rounds)
@@ -161,7 +163,7 @@ def main():
                        "vertices": n, "distinct_edges": nnz, "rounds_per_step": 1,
                        "parallelism": f"rows dealt over {world} GPUs, chunked RCCL p2p "
                                       f"exchange of x' overlapped with the row launch"
-                                      + (" (sparse: referenced entries only)" if world >= 4 else "")
+                                      + (" (sparse: referenced entries only)" if sparse_x else "")
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
