@@ -37,8 +37,11 @@ def _port() -> int:
 
 
 @pytest.mark.skipif(_gpus() < 2, reason="needs 2 GPUs (RCCL rejects two ranks on one device)")
-def test_rccl_two_ranks_match_one_rank(engine_mod, oracle_mod, tmp_path):
+@pytest.mark.parametrize("sparse", ["0", "1"])
+def test_rccl_two_ranks_match_one_rank(engine_mod, oracle_mod, tmp_path, monkeypatch, sparse):
+    """sparse = 1 forces the sparse x' exchange (its RCCL count check, packed send/recv)."""
     P, O = engine_mod, oracle_mod
+    monkeypatch.setenv("PR_SPARSE_X", sparse)
     a, m = G.wiki_text(seed=3, pages=20_000, arcs_target=200_000)
     (tmp_path / "arcs").write_bytes(a)
     (tmp_path / "map").write_bytes(m)
