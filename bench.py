@@ -140,8 +140,7 @@ def main():
     kms = st["ms_spmv_kernel"]
     achieved = bytes_launch / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = load_traffic(a.traffic_json, f"{workload}-p{world}")
-    sx_env = int(os.environ.get("PR_SPARSE_X", "-1"))   # the engine's rule (api.cpp want_sx)
-    sparse_x = world > 1 and (sx_env > 0 or (sx_env < 0 and world >= 4))
+    sparse_x = world > 1 and os.environ.get("PR_SPARSE_X", "1") != "0"  # api.cpp want_sx
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(eng, a.cpu_rounds)

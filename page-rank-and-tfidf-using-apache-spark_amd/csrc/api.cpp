@@ -103,12 +103,13 @@ int need_comm(pr_ctx* c) {
   return PR_OK;
 }
 
-// Sparse x' exchange (PR_SPARSE_X: -1 = from 4 ranks on, 0 = off, 1 = on): only the x'
-// entries a peer's edges reference travel (at p = 8 about 55 % of a slot).
+// Sparse x' exchange (PR_SPARSE_X: 1 = on, the default; 0 = the dense slot exchange): only
+// the x' entries a peer's edges reference travel (scale 26: 86 % of a slot at p = 2, 70 % at
+// p = 4, 55 % at p = 8).
 bool want_sx(const pr_ctx* c) {
-  int v = -1;
+  int v = 1;
   if (const char* e = getenv("PR_SPARSE_X")) v = atoi(e);
-  return c->opts.n_ranks > 1 && (v > 0 || (v < 0 && c->opts.n_ranks >= 4));
+  return c->opts.n_ranks > 1 && v != 0;
 }
 
 // RCCL ranks: build the lists, then check once that every rank's receive counts equal its
