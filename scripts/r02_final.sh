@@ -7,6 +7,7 @@ mkdir -p gpurun_out
 ( while sleep 50; do date >> gpurun_out/heartbeat.log; done ) &
 hb=$!
 trap 'kill $hb 2>/dev/null' EXIT
+scripts/gpu_step.sh smoke_$tag 200 python3 -c "import __graft_entry__ as g; g.smoke()" || exit $?
 scripts/gpu_step.sh pytest_$tag 700 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit $?
 scripts/gpu_step.sh bench_$tag 300 python3 bench.py || exit $?
 scripts/gpu_step.sh soak_$tag 400 python3 -u scripts/soak.py 60 || exit $?
