@@ -107,8 +107,10 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    if a.warmup > 0:
-        eng.run(a.warmup)
+    # (at p > 1 the first exchanged run builds and cross-checks the sparse-exchange lists:
+    # at least one untimed round, whatever --warmup says)
+    if a.warmup > 0 or world > 1:
+        eng.run(max(a.warmup, 1 if world > 1 else 0))
     barrier()
     t1 = time.perf_counter()
     st = eng.run(a.steps)
