@@ -258,6 +258,19 @@ def test_sparse_exchange_bit_identical(P, O, monkeypatch, p, tiny):
     parity.assert_ranks_close(out[1], O.Graph.from_rmat(16, 16, 37).run(9)["ranks"])
 
 
+@pytest.mark.parametrize("p,scale,ef", [(8, 9, 2), (5, 11, 4), (7, 12, 8), (6, 8, 1)])
+def test_sparse_exchange_small_graphs(P, O, p, scale, ef):
+    """Sparse exchange corner cases: many (chunk, peer) lists empty (tiny graphs at 8 ranks),
+    and rank counts that do not divide 8 (plain x layout): ranks vs the oracle."""
+    exp = O.Graph.from_rmat(scale, ef, 41).run(7)["ranks"]
+    grp = P.LocalGroup(p)
+    grp.each("generate_rmat", scale, ef, 41)
+    grp.run(7)
+    got = grp.members[0].ranks()
+    grp.close()
+    parity.assert_ranks_close(got, exp)
+
+
 def test_convergence_mode(P, O):
     g = O.Graph.from_rmat(14, 16, 3)
     eng = P.Engine()
