@@ -886,9 +886,11 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
         for (uint32_t i = 2u * static_cast<uint32_t>(lane); i < wn; i += 128u) {
           if (i + 1u < wn) {
             const d2v pr = *reinterpret_cast<const d2v*>(stg + i);
-            __builtin_nontemporal_store(pr, reinterpret_cast<d2v*>(part + tp0 + w0 + i));
+            if constexpr (NT >= 2) __builtin_nontemporal_store(pr, reinterpret_cast<d2v*>(part + tp0 + w0 + i));
+            else *reinterpret_cast<d2v*>(part + tp0 + w0 + i) = pr;
           } else {
-            __builtin_nontemporal_store(stg[i], part + tp0 + w0 + i);
+            if constexpr (NT >= 2) __builtin_nontemporal_store(stg[i], part + tp0 + w0 + i);
+            else part[tp0 + w0 + i] = stg[i];
           }
         }
       } else if (!(A.dbg & 1u))
@@ -2450,11 +2452,13 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   static bool lattr = false;
   if (!lattr) {
     for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true>),
-                          reinterpret_cast<const void*>(&spmv_stream<2, true, true, 0, true>)})
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, true, 0, true>),
+                          reinterpret_cast<const void*>(&spmv_stream<0, true, false, 0, true>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     lattr = true;
   }
-  if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
+  if (g->tune.nt == 0 && split && lean && !st) hipLaunchKernelGGL((spmv_stream<0, true, false, 0, true>), gr, bl, lds, s, A);
+  else if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
   else if (split && st && lean) hipLaunchKernelGGL((spmv_stream<2, true, true, 0, true>), gr, bl, lds, s, A);
   else if (split && lean) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true>), gr, bl, lds, s, A);
   else if (split && st) hipLaunchKernelGGL((spmv_stream<2, true, true>), gr, bl, lds, s, A);
