@@ -28,6 +28,7 @@
 
 #include "engine.h"
 #include "prmi355x.h"
+#include "sa_round.h"
 
 namespace prmi {
 
@@ -116,45 +117,10 @@ __device__ __forceinline__ void wave_accum_sa(uint64_t* lds_wave, int base, int 
   }
 }
 
-// Correct rounding of a superaccumulator (limbs hold 32-bit chunks plus carries).
-__device__ double sa_to_double_dev(const uint64_t* limb) {
-  uint32_t c[SA_LIMBS + 2];
-  uint64_t carry = 0;
-  for (int i = 0; i < SA_LIMBS; ++i) {
-    const uint64_t t = limb[i] + carry;
-    c[i] = static_cast<uint32_t>(t);
-    carry = t >> 32;
-  }
-  c[SA_LIMBS] = static_cast<uint32_t>(carry);
-  c[SA_LIMBS + 1] = static_cast<uint32_t>(carry >> 32);
-  int top = -1;
-  for (int i = SA_LIMBS + 1; i >= 0; --i)
-    if (c[i]) {
-      top = i * 32 + 31 - __clz(c[i]);
-      break;
-    }
-  if (top < 0) return 0.0;
-  auto bit = [&](int p) -> uint32_t { return p < 0 ? 0u : ((c[p >> 5] >> (p & 31)) & 1u); };
-  if (top < 53) {
-    uint64_t m = 0;
-    for (int p = top; p >= 0; --p) m = (m << 1) | bit(p);
-    return ldexp(static_cast<double>(m), SA_BASE_EXP);
-  }
-  uint64_t m = 0;
-  for (int p = top; p > top - 53; --p) m = (m << 1) | bit(p);
-  int lowest = top - 52;
-  const uint32_t rb = bit(lowest - 1);
-  uint32_t sticky = 0;
-  for (int p = lowest - 2; p >= 0 && !sticky; --p) sticky |= bit(p);
-  if (rb && (sticky || (m & 1))) {
-    m += 1;
-    if (m == (1ull << 53)) {
-      m >>= 1;
-      lowest += 1;
-    }
-  }
-  return ldexp(static_cast<double>(m), lowest + SA_BASE_EXP);
-}
+// Correct rounding of a superaccumulator (limbs hold 32-bit chunks plus carries): the
+// register-only form of sa_round.h (checked bit for bit against the bit-loop form on the CPU)
+static_assert(SA_LIMBS == SA_NLIMBS && SA_BASE_EXP == SA_EXP0, "sa_round.h limb layout");
+__device__ __forceinline__ double sa_to_double_dev(const uint64_t* limb) { return sa_round_fast(limb); }
 
 // =======================================================================================
 // the round: slice streams (per-piece partial sums) + fused row launch (combine + epilogue)
