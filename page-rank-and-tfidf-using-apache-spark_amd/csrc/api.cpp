@@ -1050,10 +1050,8 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
     hipEvent_t e0 = t <= nk ? c->kev[2 * (t - 1)] : nullptr;
     hipEvent_t e1 = t <= nk ? c->kev[2 * (t - 1) + 1] : nullptr;
     if (p == 1) {
-      rc = prmi::dev_round_compute(g, t, mode, c->stream, e0, e1);
-      if (rc) return fail(c, rc, "round compute");
-      rc = prmi::dev_round_finalize(g, t, tracked, c->stream);
-      if (rc) return fail(c, rc, "round finalize");
+      rc = prmi::dev_round_single(g, t, mode, tracked, c->stream, e0, e1);
+      if (rc) return fail(c, rc, "round");
     } else {
       // Chunked exchange replacing the reduceByKey shuffle (PageRank.java:139): the row
       // launch runs in chunks of class-A row blocks; as chunk k's x' slot pieces are final,

@@ -221,6 +221,9 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
 int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0);
 int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipStream_t s);
 int dev_round_reduce(DevGraph* g, hipStream_t s, hipEvent_t ev1);
+// p = 1: the whole round (stream, rows, then record reduction + finalize in one launch).
+int dev_round_single(DevGraph* g, int t, int mode, bool tracked, hipStream_t s, hipEvent_t ev0,
+                     hipEvent_t ev1);
 // Chunked x' exchange: chunk k = class-A row blocks [b0, b1) of this rank + the slot-relative
 // pieces (offset, count) its rows complete; pieces are identical on every rank.
 struct XPiece {

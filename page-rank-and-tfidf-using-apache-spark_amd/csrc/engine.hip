@@ -875,9 +875,10 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   }
 }
 
-// Sum the NSHARD shards into one record and clear them for the next round.
-__global__ __launch_bounds__(BLOCK) void reduce_shards(uint64_t* shards, uint64_t* rec) {
-  __shared__ uint64_t part[8][REC_WORDS];
+// Sum the NSHARD shards into one record and clear them for the next round (one 256-thread
+// workgroup; `out`, when given, is an LDS copy of the record for a fused finalize).
+__device__ __forceinline__ void reduce_shards_body(uint64_t* shards, uint64_t* rec, uint64_t (*part)[REC_WORDS],
+                                                   uint64_t* out) {
   const int w = threadIdx.x & 31, g = threadIdx.x >> 5;
   uint64_t s = 0;
   for (int i = g * (NSHARD / 8); i < (g + 1) * (NSHARD / 8); ++i) {
@@ -891,43 +892,77 @@ __global__ __launch_bounds__(BLOCK) void reduce_shards(uint64_t* shards, uint64_
     uint64_t t = 0;
     for (int k = 0; k < 8; ++k) t += part[k][threadIdx.x];
     rec[threadIdx.x] = t;
+    if (out) out[threadIdx.x] = t;
   }
 }
 
+__global__ __launch_bounds__(BLOCK) void reduce_shards(uint64_t* shards, uint64_t* rec) {
+  __shared__ uint64_t part[8][REC_WORDS];
+  reduce_shards_body(shards, rec, part, nullptr);
+}
+
 // Combine the p rank records (integer sums: order-free, exact) -> next round's addthis.
-__global__ void finalize_round(const uint64_t* rec_all, int p, int t, uint64_t n_tot,
-                               uint32_t extra_pages, double r0, int tracked, IterState* st) {
-  if (threadIdx.x != 0) return;
-  uint64_t dsum[SA_LIMBS] = {0}, res[SA_LIMBS] = {0}, rsum[SA_LIMBS] = {0};
-  uint64_t dcnt = 0;
-  for (int r = 0; r < p; ++r) {
-    const uint64_t* q = rec_all + r * REC_WORDS;
-    for (int i = 0; i < SA_LIMBS; ++i) {
-      dsum[i] += q[REC_DSUM + i];
-      res[i] += q[REC_RESID + i];
-      rsum[i] += q[REC_RSUM + i];
+// Run by one full wave: lanes 0 / 1 / 2 sum and round the dangling mass / residual / rank sum
+// side by side (the three roundings were serial on one thread before).
+__device__ __forceinline__ void finalize_wave(const uint64_t* rec_all, int p, int t, uint64_t n_tot,
+                                              uint32_t extra_pages, double r0, int tracked, IterState* st) {
+  const int lane = threadIdx.x & 63;
+  double v = 0.0;
+  if (lane < (tracked ? 3 : 1)) {
+    const int off = lane == 0 ? REC_DSUM : (lane == 1 ? REC_RESID : REC_RSUM);
+    uint64_t acc[SA_LIMBS];
+#pragma unroll
+    for (int i = 0; i < SA_LIMBS; ++i) acc[i] = 0;
+    for (int r = 0; r < p; ++r) {
+      const uint64_t* q = rec_all + r * REC_WORDS + off;
+#pragma unroll
+      for (int i = 0; i < SA_LIMBS; ++i) acc[i] += q[i];
     }
-    dcnt += q[REC_DCNT];
+    if (lane == 1) {
+      // round 1: the pages that are not rows drop from r0 to undefined, |dr| = r0 each
+      uint32_t c0, c1, c2, c3;
+      const int li = sa_chunks(r0, extra_pages, c0, c1, c2, c3);
+      if (li >= 0) {
+        const uint32_t cs[4] = {c0, c1, c2, c3};
+#pragma unroll
+        for (int i = 0; i < SA_LIMBS; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (i == li + q) acc[i] += cs[q];
+      }
+    }
+    v = sa_to_double_dev(acc);
   }
+  const double a = __shfl(v, 0), ra = __shfl(v, 1), rs = __shfl(v, 2);
+  if (lane != 0) return;
+  uint64_t dcnt = 0;
+  for (int r = 0; r < p; ++r) dcnt += rec_all[r * REC_WORDS + REC_DCNT];
   // :135  accum.setValue(sum / totalVertices)
-  st->a = sa_to_double_dev(dsum) / static_cast<double>(n_tot);
+  st->a = a / static_cast<double>(n_tot);
   st->dcnt = dcnt;
   if (dcnt == 0 && st->err_iter == 0) st->err_iter = t + 1;
   if (tracked) {
-    // round 1: the pages that are not rows drop from r0 to undefined, |dr| = r0 each
-    uint32_t c0, c1, c2, c3;
-    const int li = sa_chunks(r0, extra_pages, c0, c1, c2, c3);
-    if (li >= 0) {
-      const uint32_t cs[4] = {c0, c1, c2, c3};
-      for (int q = 0; q < 4 && li + q < SA_LIMBS; ++q) res[li + q] += cs[q];
-    }
-    const double ra = sa_to_double_dev(res);
-    const double rs = sa_to_double_dev(rsum);
     st->resid_abs = ra;
     st->rank_sum = rs;
     st->resid = rs > 0.0 ? ra / rs : 0.0;
   }
   st->iter = t;
+}
+
+__global__ __launch_bounds__(64) void finalize_round(const uint64_t* rec_all, int p, int t, uint64_t n_tot,
+                                                     uint32_t extra_pages, double r0, int tracked, IterState* st) {
+  finalize_wave(rec_all, p, t, n_tot, extra_pages, r0, tracked, st);
+}
+
+// p = 1: the record reduction and the finalize in one launch (one launch gap less per round).
+__global__ __launch_bounds__(BLOCK) void reduce_finalize(uint64_t* shards, uint64_t* rec, int t, uint64_t n_tot,
+                                                         uint32_t extra_pages, double r0, int tracked,
+                                                         IterState* st) {
+  __shared__ uint64_t part[8][REC_WORDS];
+  __shared__ uint64_t tot[REC_WORDS];
+  reduce_shards_body(shards, rec, part, tot);
+  __syncthreads();
+  if (threadIdx.x < 64) finalize_wave(tot, 1, t, n_tot, extra_pages, r0, tracked, st);
 }
 
 // Large launches (edge counts reach 2^32 at R-MAT scale 28) loop over blocks: every thread of
@@ -2595,6 +2630,21 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
   if (!rc) rc = dev_round_rows(g, t, mode, 0, g->nb_rows, s);
   if (!rc) rc = dev_round_reduce(g, s, ev1);
   return rc;
+}
+
+int dev_round_single(DevGraph* g, int t, int mode, bool tracked, hipStream_t s, hipEvent_t ev0,
+                     hipEvent_t ev1) {
+  std::string* err = nullptr;
+  if (g->p != 1) return PR_E_ARG;
+  int rc = dev_round_stream(g, t, s, ev0);
+  if (!rc) rc = dev_round_rows(g, t, mode, 0, g->nb_rows, s);
+  if (rc) return rc;
+  if (ev1) HIPTRY(hipEventRecord(ev1, s));
+  const uint32_t extra = (t == 1 && g->rank == 0 && !g->seeded) ? g->n - g->R : 0u;  // as dev_round_finalize
+  hipLaunchKernelGGL(reduce_finalize, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local, t, g->n_tot, extra,
+                     g->r0, tracked ? 1 : 0, g->state);
+  HIPTRY(hipGetLastError());
+  return PR_OK;
 }
 
 // Exchange plan of the chunked x' exchange (p > 1): chunk k covers the slot positions
