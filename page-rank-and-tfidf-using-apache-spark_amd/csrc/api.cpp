@@ -1022,15 +1022,12 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
     HIPCHK(c, hipEventCreate(&e));
     c->kev.push_back(e);
   }
-  rc = prmi::dev_reset_state(g, c->stream);
-  if (rc) return fail(c, rc, "reset state");
-  HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
   int done = iterations;
   prmi::IterState hs{};
   const int p = c->opts.n_ranks;
   std::vector<prmi::XChunk> plan;
   bool sx = false;  // sparse x' exchange this run
-  if (p > 1) {
+  if (p > 1) {  // (before ev_start: list building and its collectives are set-up, not rounds)
     rc = ensure_xchg(c);
     if (rc) return rc;
     plan = prmi::dev_exchange_plan(g, c->xchunks);
@@ -1044,6 +1041,9 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       if (rc) return rc;
     }
   }
+  rc = prmi::dev_reset_state(g, c->stream);
+  if (rc) return fail(c, rc, "reset state");
+  HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
   for (int t = 1; t <= iterations; ++t) {
     const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
     prmi::Span round("prmi:round");

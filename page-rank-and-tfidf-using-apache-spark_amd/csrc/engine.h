@@ -94,6 +94,11 @@ struct Tuning {
   int l2w = 4;          // PR_L2W: waves per stream workgroup dedicated to the L2 group
                         // (of 16; 0 = L2 tasks shared out over the LDS phases as in round 1;
                         // 2/3/4/5/6/8 measured at scale 26, 3-4 best)
+  uint32_t dpull = 0;   // PR_DPULL: direct-pull experiment for rows below this in-degree
+                        // (timing only, single rank; engine.hip spmv_dpull)
+  uint32_t dropdeg = 0; // PR_DROPDEG: rows below this in-degree leave the streams (timing only)
+  int l2late = 0;       // PR_L2LATE: L2-role waves prefetch the next task's columns after
+                        // their gathers instead of before (see StreamArgs::l2late)
   int lean = 1;         // PR_LEAN: 1 = the lean per-task instruction stream of the stream launch
                         // (fma-form piece sums, DPP-masked scans, SDWA LDS addresses: -11 %
                         // VALU instructions, time unchanged), 0 = the earlier form; both
@@ -190,8 +195,14 @@ struct DevGraph {
   uint32_t nb_rows = 0, nb_rows_a = 0, n_streams = 0;
   uint32_t row_rb = 1024;          // rows per row-launch block
   uint32_t row_nbH = 0, row_rbH = 256, row_lH = 0;  // heavy row blocks (first lH rows)
+  // direct-pull experiment (PR_DPULL): column-major 64-row groups of the low in-degree rows
+  uint32_t* dp_ell = nullptr;      // [dp_gbase[dp_groups]] x positions, PAD_COL padding
+  uint32_t* dp_gbase = nullptr;    // [dp_groups + 1] first slot of each group
+  double* dp_out = nullptr;        // [64 * dp_groups] the sums (a side array: not the ranks)
+  uint32_t dp_groups = 0;
   Tuning tune;
 };
+
 
 struct BuildInput {
   uint32_t n = 0;

@@ -408,6 +408,10 @@ struct StreamArgs {
                              // L2 tasks are shared out over the LDS phases, see l2mode)
   uint32_t wgdyn;            // PR_WGDYN: LDS waves claim their workgroup's tasks from an LDS
                              // counter (1) or take them round-robin (0)
+  uint32_t l2late;           // PR_L2LATE: the L2-role waves issue the next task's column loads
+                             // after their sixteen gathers have landed instead of before them
+                             // (vmcnt counts in order: gathers issued behind the prefetch wait
+                             // for it), A/B switch
 };
 constexpr int STREAM_BLOCK = 1024;
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
@@ -735,7 +739,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       if (A.dbg & 4u) b = 0;
       if (lane == 0) b |= 1u;  // a task always starts a piece
       // next task's stream words first: they stay in flight while this task gathers
-      if (un < nu) fetch_u(un);
+      const bool late = l2role && A.l2late == 1u;
+      if (un < nu && !late) fetch_u(un);
       const uint32_t unn = dyn ? (un < nu ? claim() : nu) : un + nw;
       double v[EPL];
       if (lds_task) {
@@ -776,6 +781,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
         } else {
           gather16(v, qo, gm, xr);
         }
+        if (late && un < nu) fetch_u(un);
       }
     // exclusive prefix (over lanes) of the piece starts -> first piece index of this lane
     const int cnt = __popc(b);
@@ -868,6 +874,9 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+      // PR_L2LATE=2 (A/B): the L2-role waves wait for their piece stores right here; the cost
+      // bounds what the gathers' in-order wait can lose to stores still in flight
+      if (l2role && A.l2late == 2u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       u = un;
       un = unn;
     }
@@ -1269,11 +1278,17 @@ struct NotDropped {
   __device__ __host__ bool operator()(uint64_t k) const { return k != DROP_KEY; }
 };
 __global__ void k_stream_keys(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv,
-                              Layout L, StreamGeo G, uint64_t* out) {
+                              Layout L, StreamGeo G, uint64_t* out, const uint32_t* indeg,
+                              uint32_t dropdeg) {
   PRMI_BLOCK_LOOP(nnz) {
     const uint64_t e = blk_ * blockDim.x + threadIdx.x;
     if (e >= nnz) continue;
     const uint64_t k = uk[e];
+    // PR_DROPDEG (timing only, wrong ranks): rows below this in-degree leave the streams
+    if (dropdeg && indeg[static_cast<uint32_t>(k >> nb)] < dropdeg) {
+      out[e] = DROP_KEY;
+      continue;
+    }
     const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
     const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
     uint32_t sl, q, seg, qin;
@@ -1552,6 +1567,110 @@ __global__ void k_count_heavy(const uint32_t* perm, const uint32_t* indeg, uint3
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(cnt, static_cast<unsigned>(__popcll(m)));
 }
 
+// ---- direct-pull experiment (PR_DPULL = D, timing only; single rank) ------------------------
+// Rows with in-degree < D (a suffix of the class-A rows and a suffix of the class-B rows: rows
+// are in-degree sorted) leave nothing in the streams when PR_DROPDEG = D is set as well, and a
+// thread per row sums x over the row's sources straight through the L1 / L2 instead.  Their
+// columns are stored per group of 64 consecutive rows, column-major (entry k of lane l at
+// base + 64 k + l, padded to the group's longest row with PAD_COL, whose gather reads 0), so
+// a wave reads them fully coalesced.  The sums go to a side array: this measures what such a
+// path costs, it does not feed the ranks.
+struct DpGeo {
+  uint32_t lAdp, lA, lBdp, lrows;  // direct-pull rows: [lAdp, lA) and [lBdp, lrows)
+};
+__device__ __forceinline__ uint32_t dp_of_row(const DpGeo& D, uint32_t l) {
+  if (l >= D.lAdp && l < D.lA) return l - D.lAdp;
+  if (l >= D.lBdp && l < D.lrows) return (D.lA - D.lAdp) + (l - D.lBdp);
+  return 0xFFFFFFFFu;
+}
+__device__ __forceinline__ uint32_t row_of_dp(const DpGeo& D, uint32_t i) {
+  const uint32_t na = D.lA - D.lAdp;
+  return i < na ? D.lAdp + i : D.lBdp + (i - na);
+}
+__global__ void k_count_ge(const uint32_t* perm, const uint32_t* indeg, uint32_t l0, uint32_t l1,
+                           Layout L, uint32_t thr, unsigned* cnt) {
+  const uint32_t l = l0 + blockIdx.x * blockDim.x + threadIdx.x;
+  const bool h = l < l1 && indeg[perm[row_of(L, l)]] >= thr;
+  const uint64_t m = __ballot(h);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(cnt, static_cast<unsigned>(__popcll(m)));
+}
+// in-degree of every direct-pull row and 64 x the longest row of each 64-row group
+__global__ void k_dp_deg(const uint32_t* perm, const uint32_t* indeg, DpGeo D, Layout L,
+                         uint32_t ndp, uint32_t* deg, uint32_t* gw) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t d = i < ndp ? indeg[perm[row_of(L, row_of_dp(D, i))]] : 0u;
+  if (i < ndp) deg[i] = d;
+  const int mx = wave_max_i(static_cast<int>(d));
+  if ((threadIdx.x & 63) == 0 && i < ndp) gw[i >> 6] = 64u * static_cast<uint32_t>(mx);
+}
+// (direct-pull row << 32 | x position) of every edge into such a row, appended in any order
+__global__ void k_dp_keys(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv,
+                          const uint32_t* indeg, Layout L, DpGeo D, uint32_t thr, uint64_t* out,
+                          unsigned long long* cnt) {
+  PRMI_BLOCK_LOOP(nnz) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    uint64_t key = DROP_KEY;
+    if (e < nnz) {
+      const uint64_t k = uk[e];
+      const uint32_t dv = static_cast<uint32_t>(k >> nb);
+      if (indeg[dv] < thr) {
+        const uint32_t i = dp_of_row(D, local_of(L, inv[dv]));
+        const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
+        if (i != 0xFFFFFFFFu) key = (static_cast<uint64_t>(i) << 32) | xpos(L, ks);
+      }
+    }
+    const bool take = key != DROP_KEY;
+    const uint64_t m = __ballot(take);
+    if (!m) continue;
+    unsigned long long base = 0;
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) base = atomicAdd(cnt, static_cast<unsigned long long>(__popcll(m)));
+    base = __shfl(base, 0);
+    if (take) out[base + __popcll(m & ((1ull << lane) - 1ull))] = key;
+  }
+}
+__global__ void k_dp_fill(const uint64_t* key, uint64_t ne, const uint32_t* rowstart,
+                          const uint32_t* gbase, uint32_t* ell) {
+  PRMI_BLOCK_LOOP(ne) {
+    const uint64_t e = blk_ * blockDim.x + threadIdx.x;
+    if (e >= ne) continue;
+    const uint32_t i = static_cast<uint32_t>(key[e] >> 32);
+    const uint32_t k = static_cast<uint32_t>(e) - rowstart[i];
+    ell[gbase[i >> 6] + 64u * k + (i & 63u)] = static_cast<uint32_t>(key[e]);
+  }
+}
+// one wave per 64-row group, lane = row; eight gathers in flight per lane
+__global__ __launch_bounds__(BLOCK) void spmv_dpull(const uint32_t* __restrict__ ell,
+                                                    const uint32_t* __restrict__ gbase,
+                                                    const double* x, uint32_t x_bytes,
+                                                    uint32_t ngroups, double* __restrict__ out) {
+  const uint32_t g = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  if (g >= ngroups) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t b0 = gbase[g], W = (gbase[g + 1] - b0) >> 6;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(x), static_cast<short>(0), static_cast<int>(x_bytes), 0x00020000);
+  const uint32_t* e = ell + b0 + lane;
+  double c = 0.0;
+  uint32_t k = 0;
+  auto gat = [&](uint32_t col) -> double {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(xr, col * 8u, 0, 0);  // PAD_COL: out of range, 0
+    return __longlong_as_double(static_cast<long long>((static_cast<uint64_t>(v[1]) << 32) | v[0]));
+  };
+  for (; k + 8 <= W; k += 8) {
+    uint32_t cc[8];
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) cc[u] = e[64u * (k + u)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = gat(cc[u]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c += v[u];
+  }
+  for (; k < W; ++k) c += gat(e[64u * k]);
+  out[g * 64u + lane] = c;
+}
+
 // per-piece row offset in its block + run starts T[block][stream] (sentinel where empty)
 __global__ void k_runs(const uint32_t* prow, const uint32_t* pstream, uint64_t np, RowBlocks B,
                        uint16_t* roff, uint32_t* T, uint32_t* sstart) {
@@ -1754,6 +1873,7 @@ void dev_free(DevGraph* g) {
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
   F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->mapw);
   F(g->x_seed); F(g->r_seed);
+  F(g->dp_ell); F(g->dp_gbase); F(g->dp_out);
   const int p = g->p, rank = g->rank;
   *g = DevGraph();
   g->p = p;
@@ -1805,6 +1925,9 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   T.l2mode = env_int("PR_L2MODE", T.l2mode);
   T.l2w = std::max(0, std::min(12, env_int("PR_L2W", T.l2w)));
+  T.l2late = env_int("PR_L2LATE", T.l2late);
+  T.dpull = static_cast<uint32_t>(std::max(0, env_int("PR_DPULL", 0)));
+  T.dropdeg = static_cast<uint32_t>(std::max(0, env_int("PR_DROPDEG", 0)));
   const uint32_t n = in.n;
   const uint64_t m = in.m;
   g->n = n;
@@ -2043,7 +2166,76 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&d_cnt, 2 + NG, err));
   HIPTRY(hipMemsetAsync(d_cnt, 0, 16, s));
   HIPTRY(hipMemsetAsync(d_cnt + 2, 0xFF, 8ull * NG, s));
-  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, lk_in);
+  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, lk_in, g->indeg, T.dropdeg);
+  if (T.dpull && p == 1 && nnz && lrows) {
+    // direct-pull experiment: the column-major row groups of the rows below T.dpull
+    span.next("prmi:build:direct-pull rows");
+    unsigned* hc = nullptr;
+    TRY(dmalloc(&hc, 2, err));
+    HIPTRY(hipMemsetAsync(hc, 0, 8, s));
+    if (g->lA) hipLaunchKernelGGL(k_count_ge, dim3(grid_for(g->lA)), dim3(BLOCK), 0, s, g->perm, g->indeg, 0u, g->lA, L, T.dpull, hc);
+    if (lrows > g->lA) hipLaunchKernelGGL(k_count_ge, dim3(grid_for(lrows - g->lA)), dim3(BLOCK), 0, s, g->perm, g->indeg, g->lA, lrows, L, T.dpull, hc + 1);
+    unsigned nge[2] = {0, 0};
+    HIPTRY(hipMemcpyAsync(nge, hc, 8, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(hc);
+    const DpGeo D{nge[0], g->lA, g->lA + nge[1], lrows};
+    const uint32_t ndp = (D.lA - D.lAdp) + (D.lrows - D.lBdp), ngr = (ndp + 63) / 64;
+    if (ndp) {
+      uint32_t *deg = nullptr, *rowstart = nullptr, *gw = nullptr;
+      TRY(dmalloc(&deg, ndp + 1ull, err));
+      TRY(dmalloc(&rowstart, ndp + 1ull, err));
+      TRY(dmalloc(&gw, ngr + 1ull, err));
+      TRY(dmalloc(&g->dp_gbase, ngr + 1ull, err));
+      HIPTRY(hipMemsetAsync(deg, 0, 4ull * (ndp + 1), s));
+      HIPTRY(hipMemsetAsync(gw, 0, 4ull * (ngr + 1), s));
+      hipLaunchKernelGGL(k_dp_deg, dim3(grid_for(ndp)), dim3(BLOCK), 0, s, g->perm, g->indeg, D, L, ndp, deg, gw);
+      size_t tb = 0;
+      HIPTRY(rocprim::exclusive_scan(nullptr, tb, deg, rowstart, 0u, ndp + 1ull, rocprim::plus<uint32_t>(), s));
+      TRY(tmp.ensure(tb, err));
+      HIPTRY(rocprim::exclusive_scan(tmp.p, tb, deg, rowstart, 0u, ndp + 1ull, rocprim::plus<uint32_t>(), s));
+      HIPTRY(rocprim::exclusive_scan(nullptr, tb, gw, g->dp_gbase, 0u, ngr + 1ull, rocprim::plus<uint32_t>(), s));
+      TRY(tmp.ensure(tb, err));
+      HIPTRY(rocprim::exclusive_scan(tmp.p, tb, gw, g->dp_gbase, 0u, ngr + 1ull, rocprim::plus<uint32_t>(), s));
+      uint32_t ne = 0, nell = 0;
+      HIPTRY(hipMemcpyAsync(&ne, rowstart + ndp, 4, hipMemcpyDeviceToHost, s));
+      HIPTRY(hipMemcpyAsync(&nell, g->dp_gbase + ngr, 4, hipMemcpyDeviceToHost, s));
+      HIPTRY(hipStreamSynchronize(s));
+      uint64_t *dk = nullptr, *dk2 = nullptr;
+      unsigned long long* dc = nullptr;
+      TRY(dmalloc(&dk, ne, err));
+      TRY(dmalloc(&dk2, ne, err));
+      TRY(dmalloc(&dc, 1, err));
+      HIPTRY(hipMemsetAsync(dc, 0, 8, s));
+      hipLaunchKernelGGL(k_dp_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, g->indeg, L, D, T.dpull, dk, dc);
+      unsigned long long got = 0;
+      HIPTRY(hipMemcpyAsync(&got, dc, 8, hipMemcpyDeviceToHost, s));
+      HIPTRY(hipStreamSynchronize(s));
+      (void)hipFree(dc);
+      if (got != ne) {
+        if (err) *err = "direct-pull rows: edge count mismatch";
+        return PR_E_HIP;
+      }
+      rocprim::double_buffer<uint64_t> db(dk, dk2);
+      HIPTRY(rocprim::radix_sort_keys(nullptr, tb, db, ne, 0, 64, s));
+      TRY(tmp.ensure(tb, err));
+      if (ne) HIPTRY(rocprim::radix_sort_keys(tmp.p, tb, db, ne, 0, 64, s));
+      TRY(dmalloc(&g->dp_ell, nell, err));
+      TRY(dmalloc(&g->dp_out, 64ull * ngr, err));
+      HIPTRY(hipMemsetAsync(g->dp_ell, 0xFF, 4ull * std::max<uint32_t>(nell, 1), s));
+      if (ne) hipLaunchKernelGGL(k_dp_fill, dim3(grid_loop(ne)), dim3(BLOCK), 0, s, db.current(), ne, rowstart, g->dp_gbase, g->dp_ell);
+      HIPTRY(hipStreamSynchronize(s));
+      HIPTRY(hipGetLastError());
+      (void)hipFree(dk);
+      (void)hipFree(dk2);
+      (void)hipFree(deg);
+      (void)hipFree(rowstart);
+      (void)hipFree(gw);
+      g->dp_groups = ngr;
+      fprintf(stderr, "[prmi355x] direct-pull experiment: in-degree < %u: %u rows (%u class A, %u class B), %u edges, %u column slots (%.1f %% padding)\n",
+              T.dpull, ndp, D.lA - D.lAdp, D.lrows - D.lBdp, ne, nell, nell ? 100.0 * (nell - ne) / nell : 0.0);
+    }
+  }
   if (p > 1 && g->maxA) {  // sparse x' exchange: the cross-rank entries (host bitmaps)
     const uint64_t words = (static_cast<uint64_t>(p) * g->maxA + 31) / 32;
     uint32_t *sb = nullptr, *rb = nullptr;
@@ -2062,7 +2254,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   }
   uint64_t lnnz = nnz;
   uint64_t* lk_alt = uniq;  // the unique keys are dead from here: sort scratch
-  if (p > 1 && nnz) {  // keep this rank's rows' edges (order-preserving select)
+  if ((p > 1 || T.dropdeg) && nnz) {  // keep this rank's rows' edges (order-preserving select)
     size_t tb = 0;
     HIPTRY(rocprim::select(nullptr, tb, lk_in, uniq, d_cnt, nnz, NotDropped(), s));
     TRY(tmp.ensure(tb, err));
@@ -2500,6 +2692,7 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   S.stamps = dst;
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
   S.wgdyn = static_cast<uint32_t>(env_int("PR_WGDYN", 1) != 0);
+  S.l2late = static_cast<uint32_t>(g->tune.l2late);
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
@@ -2639,8 +2832,37 @@ int dev_round_single(DevGraph* g, int t, int mode, bool tracked, hipStream_t s, 
   int rc = dev_round_stream(g, t, s, ev0);
   if (!rc) rc = dev_round_rows(g, t, mode, 0, g->nb_rows, s);
   if (rc) return rc;
+  if (g->dp_groups) {  // direct-pull experiment (timing only): inside the SpMV event bracket
+    const double* x_in = t == 1 ? (g->seeded ? g->x_seed : g->x_init) : g->xbuf[t & 1];
+    hipLaunchKernelGGL(spmv_dpull, dim3((g->dp_groups + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, s,
+                       g->dp_ell, g->dp_gbase, x_in,
+                       static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull)), g->dp_groups, g->dp_out);
+    if (t == 1 && getenv("PR_DPULL_CHECK")) {  // the side sums against a host walk of the same slots
+      std::vector<uint32_t> gb(g->dp_groups + 1ull);
+      HIPTRY(hipMemcpyAsync(gb.data(), g->dp_gbase, 4ull * gb.size(), hipMemcpyDeviceToHost, s));
+      HIPTRY(hipStreamSynchronize(s));
+      std::vector<uint32_t> ell(std::max<uint32_t>(gb.back(), 1));
+      std::vector<double> xs(g->X), out(64ull * g->dp_groups);
+      HIPTRY(hipMemcpy(ell.data(), g->dp_ell, 4ull * gb.back(), hipMemcpyDeviceToHost));
+      HIPTRY(hipMemcpy(xs.data(), x_in, 8ull * g->X, hipMemcpyDeviceToHost));
+      HIPTRY(hipMemcpy(out.data(), g->dp_out, 8ull * out.size(), hipMemcpyDeviceToHost));
+      uint64_t bad = 0, nz = 0;
+      for (uint32_t gr = 0; gr < g->dp_groups; ++gr)
+        for (uint32_t l = 0; l < 64; ++l) {
+          double c = 0.0;
+          for (uint32_t k = 0; k < (gb[gr + 1] - gb[gr]) / 64; ++k) {
+            const uint32_t col = ell[gb[gr] + 64 * k + l];
+            c += col == PAD_COL ? 0.0 : xs[col];
+          }
+          bad += c != out[64ull * gr + l];
+          nz += c != 0.0;
+        }
+      fprintf(stderr, "[dpull check] %u groups, %llu nonzero row sums, %llu mismatches\n", g->dp_groups,
+              static_cast<unsigned long long>(nz), static_cast<unsigned long long>(bad));
+    }
+  }
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
-  const uint32_t extra = (t == 1 && g->rank == 0 && !g->seeded) ? g->n - g->R : 0u;  // as dev_round_finalize
+  const uint32_t extra = (t == 1 && !g->seeded) ? g->n - g->R : 0u;  // as dev_round_finalize
   hipLaunchKernelGGL(reduce_finalize, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local, t, g->n_tot, extra,
                      g->r0, tracked ? 1 : 0, g->state);
   HIPTRY(hipGetLastError());
@@ -2758,8 +2980,10 @@ int dev_round_finalize(DevGraph* g, int t, bool tracked, hipStream_t s) {
   std::string* err = nullptr;
   const uint64_t* rec = g->p > 1 ? g->rec_all : g->rec_local;
   // round 1 starts from r^0 == 1 on every page: pages that are not rows drop to 0 (|dr|=1)
-  // (a seed has no defined page outside the rows: nothing drops)
-  const uint32_t extra = (t == 1 && g->rank == 0 && !g->seeded) ? g->n - g->R : 0u;
+  // (a seed has no defined page outside the rows: nothing drops).  Every rank finalizes the
+  // same p records, so every rank adds the term: all ranks see one global residual and take
+  // the same stop decision.
+  const uint32_t extra = (t == 1 && !g->seeded) ? g->n - g->R : 0u;
   hipLaunchKernelGGL(finalize_round, dim3(1), dim3(64), 0, s, rec, g->p, t, g->n_tot, extra, g->r0, tracked ? 1 : 0, g->state);
   HIPTRY(hipGetLastError());
   return PR_OK;

@@ -253,7 +253,9 @@ class Engine:
         for t in range(1, iterations + 1):
             self._check(lib().pr_ext_round(self._h, t, _ptr(send)))
             recv = np.ascontiguousarray(allgather(send), np.uint8)
-            assert recv.size == unit.value * self.n_ranks
+            if recv.size != unit.value * self.n_ranks:
+                raise ValueError(f"allgather returned {recv.size} bytes, expected "
+                                 f"{unit.value} x {self.n_ranks} ranks")
             self._check(lib().pr_ext_complete(self._h, t, _ptr(recv), C.byref(stop)))
             if stop.value:
                 break
