@@ -177,6 +177,20 @@ int pr_graph_get_info(pr_ctx* ctx, pr_graph_info* out);
  * would die at :125 (stats->failed_iteration says which round).  Collective. */
 int pr_run(pr_ctx* ctx, int32_t iterations, double tol, pr_stats* stats);
 
+/* pr_run without allocation.  No counterpart in the reference: it exists for callers that
+ * cannot allocate device memory while they run rounds (code under HIP graph capture, tight
+ * serving loops, harnesses that forbid hipMalloc).  Same rounds, same kernels and bit-identical
+ * ranks as pr_run on a single-GPU context (n_ranks = 1), but everything a round writes besides
+ * the context's own x / rank vectors -- the per-piece partial sums, the record shards, the round
+ * record and the round state -- lives in a fixed file-scope device array (32 MiB + 66 KiB per
+ * GPU, held until the process ends) instead of the context's buffers, and the call makes no
+ * hipMalloc / hipFree (its state reset and clears are kernel launches, per-round kernel timing
+ * is off: stats->ms_spmv_kernel = 0).  Limit: graphs of at most 4 Mi piece sums per round
+ * (about 10 M distinct edges); larger ones get PR_E_ARG with the sizes in pr_last_error.
+ * Every context on one GPU shares that GPU's array: calls that overlap in time on one GPU race
+ * (calls in sequence are fine: each call resets what must start at zero). */
+int pr_run_static(pr_ctx* ctx, int32_t iterations, double tol, pr_stats* stats);
+
 /* Resume (the reference has no checkpoint).  pr_set_ranks seeds the
  * following pr_run calls with ranks by vertex id (as pr_get_ranks returns them, 0.0 =
  * undefined) reached after `rounds_done` >= 1 rounds: pr_run(T) then computes rounds

@@ -61,6 +61,8 @@ struct pr_ctx {
   double ext_tol = 0.0;
   bool ext_tracked = false;
   prmi::IterState ext_hs{};
+  // pr_run_static: this device's static scratch (resolved once in pr_create)
+  prmi::StaticScratch scratch{};
 };
 
 namespace {
@@ -495,6 +497,10 @@ int pr_create(pr_ctx** out, const pr_opts* opts) {
       return PR_E_HIP;
     }
     c->has_device = true;
+    // device address of the static scratch (pr_run_static), once per device, here at set-up;
+    // a failure only disables that entry point
+    std::string e;
+    if (prmi::dev_static_scratch(c->device, &c->scratch, &e) != PR_OK) c->scratch = prmi::StaticScratch{};
   }
   *out = c;
   return PR_OK;
@@ -1132,6 +1138,102 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   s.residual = tracked ? hs.resid : 0.0;
   s.rank_sum = tracked ? hs.rank_sum : 0.0;
   // the reduce of round err_iter saw an empty danglingMap: the reference dies there
+  if (hs.err_iter != 0 && hs.err_iter <= done) {
+    s.failed_iteration = t0 + hs.err_iter;
+    if (st) *st = s;
+    return fail(c, PR_E_EMPTY_DANGLING,
+                "java.lang.UnsupportedOperationException: empty collection (iteration " +
+                    std::to_string(t0 + hs.err_iter) + ")");
+  }
+  c->last_iters = done;
+  if (st) *st = s;
+  return PR_OK;
+}
+
+// pr_run for callers that cannot allocate: the round loop of a single-GPU context with every
+// per-round scratch array (piece sums, record shards, record, round state) in this device's
+// static scratch instead of the context's own buffers.  Same kernels, same order of sums.
+int pr_run_static(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  if (iterations < 0) return fail(c, PR_E_ARG, "iterations < 0");
+  if (c->opts.n_ranks != 1 || !c->group.empty() || c->external)
+    return fail(c, PR_E_ARG, "pr_run_static: single-GPU contexts only (n_ranks = 1)");
+  if (!c->scratch.partial) return fail(c, PR_E_HIP, "pr_run_static: the static scratch of this device could not be resolved");
+  DevGraph* g = &c->dg;
+  if (g->n_pieces > c->scratch.max_pieces)
+    return fail(c, PR_E_ARG, "pr_run_static: the graph needs " + std::to_string(g->n_pieces) +
+                                 " piece sums per round, the static scratch holds " +
+                                 std::to_string(c->scratch.max_pieces) + " (use pr_run)");
+  pr_stats s{};
+  s.nnz = g->nnz;
+  s.n_vertices = g->n;
+  s.bytes_per_iter = 4ull * g->nnz + 24ull * g->n + 8;
+  c->host_ranks_valid = false;
+  c->last_iters = -1;
+  if (iterations == 0) {
+    c->last_iters = 0;
+    if (st) *st = s;
+    return PR_OK;
+  }
+  const int t0 = g->seeded ? c->seed_rounds : 0;
+  if (!g->seeded && g->W0 == 0) {
+    s.failed_iteration = 1;
+    if (st) *st = s;
+    return fail(c, PR_E_EMPTY_DANGLING, "java.lang.UnsupportedOperationException: empty collection (iteration 1)");
+  }
+  const bool tracked = tol > 0.0 || (c->opts.flags & PR_F_TRACK_RESIDUAL);
+  // the rounds run on the context's graph with its scratch arrays swapped for the static ones
+  struct Swap {
+    DevGraph* g;
+    double* partial;
+    uint64_t *shards, *rec;
+    prmi::IterState* state;
+    ~Swap() {
+      g->partial = partial;
+      g->shards = shards;
+      g->rec_local = rec;
+      g->state = state;
+      g->no_alloc = false;
+    }
+  } swap{g, g->partial, g->shards, g->rec_local, g->state};
+  g->partial = c->scratch.partial;
+  g->shards = c->scratch.shards;
+  g->rec_local = c->scratch.rec;
+  g->state = c->scratch.state;
+  g->no_alloc = true;
+  // the scratch keeps the last call's contents: state and shards start from this launch
+  rc = prmi::dev_reset_state_kernel(g, c->stream);
+  if (rc) return fail(c, rc, "reset state");
+  HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+  int done = iterations;
+  prmi::IterState hs{};
+  for (int t = 1; t <= iterations; ++t) {
+    const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
+    rc = prmi::dev_round_single(g, t, mode, tracked, c->stream, nullptr, nullptr);
+    if (rc) return fail(c, rc, "round");
+    if (tol > 0.0) {
+      HIPCHK(c, hipMemcpyAsync(&hs, g->state, sizeof(hs), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (hs.resid <= tol) {
+        done = t;
+        break;
+      }
+    }
+  }
+  HIPCHK(c, hipEventRecord(c->ev_stop, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&hs, g->state, sizeof(hs), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  HIPCHK(c, hipEventElapsedTime(&ms, c->ev_start, c->ev_stop));
+  s.iterations = done;
+  s.ms_total = ms;
+  s.ms_per_iter = ms / done;
+  s.gteps = s.ms_per_iter > 0 ? static_cast<double>(g->nnz) / (s.ms_per_iter * 1e-3) / 1e9 : 0.0;
+  s.residual = tracked ? hs.resid : 0.0;
+  s.rank_sum = tracked ? hs.rank_sum : 0.0;
   if (hs.err_iter != 0 && hs.err_iter <= done) {
     s.failed_iteration = t0 + hs.err_iter;
     if (st) *st = s;

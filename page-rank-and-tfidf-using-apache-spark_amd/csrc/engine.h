@@ -200,9 +200,27 @@ struct DevGraph {
   uint32_t* dp_gbase = nullptr;    // [dp_groups + 1] first slot of each group
   double* dp_out = nullptr;        // [64 * dp_groups] the sums (a side array: not the ranks)
   uint32_t dp_groups = 0;
+  bool no_alloc = false;           // inside pr_run_static: nothing may allocate (no PR_STAMPS)
   Tuning tune;
 };
 
+// Static scratch of the allocation-free run (one file-scope device array per GPU, engine.hip):
+// room for the per-piece partial sums of graphs up to STATIC_SCRATCH_PIECES pieces, the record
+// shards, the round record and the round state.  32 MiB + 66 KiB per GPU, held until the
+// process ends.
+constexpr uint64_t STATIC_SCRATCH_PIECES = 4ull << 20;
+struct StaticScratch {
+  double* partial = nullptr;
+  uint64_t* shards = nullptr;
+  uint64_t* rec = nullptr;
+  IterState* state = nullptr;
+  uint64_t max_pieces = 0;
+};
+// The scratch of `device` (which must be the current device): resolves the array's device
+// address on first use per device, no allocation.
+int dev_static_scratch(int device, StaticScratch* out, std::string* err);
+// dev_reset_state through one kernel launch (no host-memory copy, no memset).
+int dev_reset_state_kernel(DevGraph* g, hipStream_t s);
 
 struct BuildInput {
   uint32_t n = 0;

@@ -2606,6 +2606,67 @@ int dev_reset_state(DevGraph* g, hipStream_t s) {
 
 double* dev_x_out(DevGraph* g, int t) { return g->xbuf[(t - 1) & 1]; }
 
+// ---- static scratch of the allocation-free run (pr_run_static) ---------------------------
+// One file-scope device array per GPU holds everything a round writes besides the graph's own
+// x / rank buffers: the per-piece partial sums, the atomic record shards, the round record and
+// the round state.  Host code never uses the array's name as an address: dev_static_scratch()
+// asks the runtime once per device (hipGetSymbolAddress, that device current) and hands out
+// that pointer.
+constexpr uint64_t SS_PARTIAL = 0;                                                     // doubles
+constexpr uint64_t SS_SHARDS = SS_PARTIAL + 8ull * STATIC_SCRATCH_PIECES;              // u64 shards
+constexpr uint64_t SS_REC = SS_SHARDS + 8ull * NSHARD * REC_WORDS;                     // u64 record
+constexpr uint64_t SS_STATE = SS_REC + 8ull * REC_WORDS;                               // IterState
+constexpr uint64_t SS_BYTES = SS_STATE + 256;
+static_assert(sizeof(IterState) <= 256, "IterState outgrew its scratch slot");
+static __device__ __align__(256) unsigned char scratch[SS_BYTES];
+
+namespace {
+constexpr int SS_MAX_DEV = 64;
+void* g_scratch_ptr[SS_MAX_DEV] = {nullptr};
+
+__global__ void k_state_set(IterState* st, IterState v, uint64_t* shards, uint32_t nwords) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *st = v;
+  if (i < nwords) shards[i] = 0;
+}
+}  // namespace
+
+int dev_static_scratch(int device, StaticScratch* out, std::string* err) {
+  if (device < 0 || device >= SS_MAX_DEV) {
+    if (err) *err = "static scratch: device ordinal out of range";
+    return PR_E_ARG;
+  }
+  if (!g_scratch_ptr[device]) {
+    void* ptr = nullptr;
+    HIPTRY(hipGetSymbolAddress(&ptr, HIP_SYMBOL(scratch)));  // (the caller made `device` current)
+    g_scratch_ptr[device] = ptr;
+  }
+  unsigned char* b = static_cast<unsigned char*>(g_scratch_ptr[device]);
+  out->partial = reinterpret_cast<double*>(b + SS_PARTIAL);
+  out->shards = reinterpret_cast<uint64_t*>(b + SS_SHARDS);
+  out->rec = reinterpret_cast<uint64_t*>(b + SS_REC);
+  out->state = reinterpret_cast<IterState*>(b + SS_STATE);
+  out->max_pieces = STATIC_SCRATCH_PIECES;
+  return PR_OK;
+}
+
+// dev_reset_state with kernels only (no copy from pageable host memory, no memset node): the
+// state travels as a kernel argument and the same launch clears the shards.
+int dev_reset_state_kernel(DevGraph* g, hipStream_t s) {
+  std::string* err = nullptr;
+  IterState st{};
+  if (g->seeded) {
+    st = g->seed_state;
+  } else {
+    st.a = g->n_tot ? (static_cast<double>(g->W0) * g->r0) / static_cast<double>(g->n_tot) : 0.0;
+    st.dcnt = g->W0;
+  }
+  const uint32_t nw = NSHARD * REC_WORDS;
+  hipLaunchKernelGGL(k_state_set, dim3((nw + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, g->state, st, g->shards, nw);
+  HIPTRY(hipGetLastError());
+  return PR_OK;
+}
+
 namespace {
 
 void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
@@ -2680,7 +2741,7 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   S.H = g->hot_h;
   S.colmask = g->tune.colmask;
   S.l2mode = static_cast<uint32_t>(g->tune.l2mode);
-  const bool stamps = t == 1 && getenv("PR_STAMPS") && g->nlds && g->ntask;
+  const bool stamps = t == 1 && !g->no_alloc && getenv("PR_STAMPS") && g->nlds && g->ntask;
   const uint32_t nph = g->nlds + ((g->tune.l2mode == 1 || g->tune.l2w) ? 1u : 0u);
   std::vector<uint64_t> hst;
   uint64_t* dst = nullptr;

@@ -143,6 +143,7 @@ def lib():
         "pr_generate_rmat": (I32, [P, I32, I32, U64]),
         "pr_graph_get_info": (I32, [P, C.POINTER(GraphInfo)]),
         "pr_run": (I32, [P, I32, D, C.POINTER(Stats)]),
+        "pr_run_static": (I32, [P, I32, D, C.POINTER(Stats)]),
         "pr_get_ranks": (I32, [P, P, U64]),
         "pr_topk": (I32, [P, U32, P, P, P, C.POINTER(U32)]),
         "pr_write_top_page": (I32, [P, C.c_char_p]),
@@ -289,6 +290,14 @@ class Engine:
     def run(self, iterations: int = 10, tol: float = 0.0) -> Dict[str, float]:
         st = Stats()
         rc = lib().pr_run(self._h, iterations, tol, C.byref(st))
+        self._check(rc)
+        return st.as_dict()
+
+    def run_static(self, iterations: int = 10, tol: float = 0.0) -> Dict[str, float]:
+        """``pr_run`` with the per-round scratch in the library's static device array: no
+        allocation during the call (single-GPU contexts, bounded graph size)."""
+        st = Stats()
+        rc = lib().pr_run_static(self._h, iterations, tol, C.byref(st))
         self._check(rc)
         return st.as_dict()
 
