@@ -8,8 +8,14 @@ stream, and an all-gather of the exact per-rank record).  The graph (R-MAT scale
 generated on the device; ~1.06e9 distinct edges) is resident in HBM before timing starts.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--no-cpu-baseline]
+                  [--exchange rccl|external] [--watchdog SECONDS]
   (N > 1: launched by torch.distributed.run, one process per GPU; RCCL over xGMI; the
-   graph is the same for every N -> strong scaling)
+   graph is the same for every N -> strong scaling.  --exchange external moves every round's
+   x slot and exact record through the gloo world instead (host-staged, pr_ext_*): the same
+   launch harness and per-rank engine work with only the transport changed, so an N-process
+   world also runs on one GPU.  At N > 1 a watchdog thread follows the rounds the device has
+   finished (pr_progress) and ends the process with a message naming the round when nothing
+   completes for --watchdog seconds.)
 
 Prints ONE JSON line on rank 0 (metric GTEPS = distinct edges / round time / 1e9).
 """
@@ -17,6 +23,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -43,7 +50,52 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rounds", type=int, default=40)   # ~10 s of host CPU work at scale 26
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--exchange", choices=("rccl", "external"), default="rccl",
+                    help="N > 1: RCCL over xGMI (one GPU per rank), or the caller-staged "
+                         "exchange over the gloo world (any number of ranks per GPU)")
+    ap.add_argument("--watchdog", type=float, default=90.0,
+                    help="N > 1: seconds without a finished round before the process exits "
+                         "with a diagnostic (0 = off)")
     return ap.parse_args()
+
+
+class Watchdog(threading.Thread):
+    """Ends the process (os._exit: a fresh exit, nothing is re-executed) when the engine's
+    round loop stops finishing rounds.  `phase` names what the main thread is doing; only the
+    phases in `watched` are timed."""
+
+    def __init__(self, eng, rank, world, exchange, limit):
+        super().__init__(daemon=True)
+        self.eng, self.rank, self.world, self.exchange, self.limit = eng, rank, world, exchange, limit
+        self.phase = "setup"
+        self.rounds = 0
+        self._stop = threading.Event()
+
+    def enter(self, phase, rounds=0):
+        self.phase, self.rounds = phase, rounds
+        self._last = (None, time.monotonic())
+
+    def stop(self):
+        self._stop.set()
+
+    def run(self):
+        self._last = (None, time.monotonic())
+        while not self._stop.wait(0.5):
+            if not self.phase.startswith("rounds"):
+                continue
+            prog = self.eng.progress()
+            now = time.monotonic()
+            if prog != self._last[0]:
+                self._last = (prog, now)
+            elif now - self._last[1] > self.limit:
+                sys.stderr.write(
+                    f"[bench watchdog] rank {self.rank}/{self.world} ({self.exchange} exchange): no "
+                    f"round finished for {self.limit:.0f} s in phase '{self.phase}' "
+                    f"({self.rounds} rounds requested): {prog[0]} rounds handed to the device, "
+                    f"{prog[1]} finished -- the exchange after round {prog[1]} did not complete "
+                    f"on this rank; exiting\n")
+                sys.stderr.flush()
+                os._exit(86)
 
 
 def cpu_baseline(eng, rounds: int):
@@ -92,12 +144,28 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)   # rendezvous only
     eng = P.Engine(n_ranks=world, rank=rank)
-    if world > 1:
+    external = world > 1 and a.exchange == "external"
+    allgather = None
+    if world > 1 and external:
+        import torch
+        eng.comm_init_external()
+
+        def allgather(send):                      # host buffers only: gloo never sees the GPU
+            t = torch.from_numpy(send)
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            return torch.cat(parts).numpy()
+    elif world > 1:
         import torch
         uid = P.comm_unique_id() if rank == 0 else bytes(128)
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
         eng.comm_init(bytes(t.tolist()))
+    comm = eng.comm_query()
+    dog = None
+    if world > 1 and a.watchdog > 0:
+        dog = Watchdog(eng, rank, world, a.exchange, a.watchdog)
+        dog.start()
     t0 = time.time()
     eng.generate_rmat(a.scale, a.edge_factor, a.seed)
     info = eng.info()
@@ -107,21 +175,40 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def rounds(k, phase):
+        if dog is not None:
+            dog.enter(phase, k)
+        st_ = eng.run_external(k, allgather) if external else eng.run(k)
+        if dog is not None:
+            dog.enter("idle")
+        return st_
+
     # (at p > 1 the first exchanged run builds and cross-checks the sparse-exchange lists:
     # at least one untimed round, whatever --warmup says)
     if a.warmup > 0 or world > 1:
-        eng.run(max(a.warmup, 1 if world > 1 else 0))
+        rounds(max(a.warmup, 1 if world > 1 else 0), "rounds (warm-up)")
     barrier()
     t1 = time.perf_counter()
-    st = eng.run(a.steps)
+    st = rounds(a.steps, "rounds (timed)")
     t2 = time.perf_counter()
     barrier()
+    if dog is not None:
+        dog.stop()
     wall = t2 - t1
+    if external:                                  # pr_ext_end reports no loop time of its own
+        st["ms_per_iter"] = wall * 1e3 / a.steps
+    exposed_rank = None
     if dist is not None:
         import torch
         w = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(w, op=dist.ReduceOp.MAX)
         wall = float(w.item())
+        # per rank: what the exchange, the record all-gather and finalize leave exposed on
+        # top of that rank's own SpMV launches
+        mine = torch.tensor([(t2 - t1) * 1e3 / a.steps - st["ms_spmv_kernel"]], dtype=torch.float64)
+        parts = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        exposed_rank = [round(max(float(x.item()), 0.0), 4) for x in parts]
         k = torch.tensor([st["ms_spmv_kernel"]], dtype=torch.float64)
         dist.all_reduce(k, op=dist.ReduceOp.MAX)
         st["ms_spmv_kernel"] = float(k.item())
@@ -142,7 +229,7 @@ def main():
     kms = st["ms_spmv_kernel"]
     achieved = bytes_launch / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = load_traffic(a.traffic_json, f"{workload}-p{world}")
-    sparse_x = world > 1 and os.environ.get("PR_SPARSE_X", "1") != "0"  # api.cpp want_sx
+    sparse_x = world > 1 and not external and os.environ.get("PR_SPARSE_X", "1") != "0"  # api.cpp want_sx
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(eng, a.cpu_rounds)
@@ -162,9 +249,12 @@ def main():
             "data": "synthetic (Graph500 R-MAT generated on device, Philox seed %d)" % a.seed,
             "config": {"workload": workload, "scale": a.scale, "edge_factor": a.edge_factor,
                        "vertices": n, "distinct_edges": nnz, "rounds_per_step": 1,
-                       "parallelism": f"rows dealt over {world} GPUs, chunked RCCL p2p "
-                                      f"exchange of x' overlapped with the row launch"
-                                      + (" (sparse: referenced entries only)" if sparse_x else "")
+                       "parallelism": (f"rows dealt over {world} ranks, x' slots and exact records "
+                                       f"all-gathered over the gloo world (host-staged, pr_ext_*)"
+                                       if external else
+                                       f"rows dealt over {world} GPUs, chunked RCCL p2p "
+                                       f"exchange of x' overlapped with the row launch"
+                                       + (" (sparse: referenced entries only)" if sparse_x else ""))
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -184,6 +274,11 @@ def main():
             # all-gather and finalize leave exposed on top of them
             "round_breakdown_ms": {"spmv_kernels": round(kms, 4),
                                    "exposed_exchange_and_finalize": round(max(ms_step - kms, 0.0), 4)},
+            # the transport the rounds used: for RCCL, ncclCommCount / ncclCommUserRank of
+            # this rank's communicator (must equal n_gpus / 0 on rank 0)
+            "exchange": {"transport": comm["transport"], "comm_ranks": comm["comm_ranks"],
+                         "comm_rank": comm["comm_rank"],
+                         "exposed_ms_per_rank": exposed_rank},
             "build_s": round(build_s, 2),
             "build_id": P.build_id(),
         }

@@ -152,6 +152,41 @@ int pr_ext_round(pr_ctx* ctx, int32_t t, void* send);
 int pr_ext_complete(pr_ctx* ctx, int32_t t, const void* recv_all, int32_t* stop);
 int pr_ext_end(pr_ctx* ctx, pr_stats* stats);
 
+/* Diagnostics (no counterpart in the reference; Spark's web UI and log4j lines play this role
+ * there).  pr_progress reports the round loop that is running or ran last on this context:
+ * rounds whose work has been handed to the device and rounds the device has finished.  It may
+ * be called from another thread while pr_run / pr_run_group block, e.g. by a watchdog that
+ * wants to name the round in which a multi-GPU exchange stopped making progress.
+ * pr_comm_query reports the transport behind a context (0 none, 1 RCCL, 2 in-process rank
+ * group, 3 caller-staged) and, for RCCL, ncclCommCount / ncclCommUserRank of its communicator. */
+int pr_progress(pr_ctx* ctx, int32_t* rounds_enqueued, int32_t* rounds_done);
+/* Self-test behind the "same graph, same bits" property of reduceByKey(Sum)'s replacement
+ * (PageRank.java:139, :208-213 leave the order of the adds open; the engine fixes it): the row
+ * launch adds a row's pieces with one LDS double-add instruction per 64 pieces, and lanes of
+ * one instruction that hit the same row are applied in an order the hardware chooses.  This
+ * call issues that instruction form with `cases` different lane / row / value patterns,
+ * `launches` times each, from 8192 waves spread over every compute unit, and compares all
+ * accumulators bit for bit: *copies = accumulator sets compared, *differing = sets that differ
+ * from the first of their pattern (0 = the order is a function of the pattern alone),
+ * *lane_order_cases = patterns whose bits equal the serial sum in ascending lane order. */
+int pr_selftest_sum_order(pr_ctx* ctx, uint32_t cases, uint32_t launches, uint64_t* copies,
+                          uint64_t* differing, uint64_t* lane_order_cases);
+int pr_comm_query(pr_ctx* ctx, int32_t* transport, int32_t* comm_ranks, int32_t* comm_rank);
+
+/* The engine's partitioner, on the host.  Spark's HashPartitioner decides which executor owns
+ * a key of the reduceByKey shuffle (PageRank.java:139) and the join at :95; here rows are dealt
+ * to ranks in chunks of 16 internal vertex ids and every source's contribution has a fixed
+ * place in the x vector (slice-major when n_ranks divides 8).  pr_layout_map evaluates the very
+ * functions the kernels use, compiled for the host (no device needed): for `count` internal
+ * vertex ids (the engine's order: class A = pages with in- and out-links [0, n_a), class B =
+ * in-links only [n_a, n_a + n_b), class C = out-links only, the next n_c) it writes the owner
+ * rank and local row of each row (0xFFFFFFFF where the id is not a row) and the x position of
+ * each column (~0 where it is not a column) as rank `rank` of `n_ranks` holds them; dims_out =
+ * {x slot length per rank, x length, local rows, local class-A rows}.  Any output may be NULL. */
+int pr_layout_map(int32_t n_ranks, int32_t rank, uint32_t n_a, uint32_t n_b, uint32_t n_c,
+                  uint64_t count, const uint32_t* internal_ids, uint32_t* owner_out,
+                  uint32_t* local_row_out, uint64_t* x_pos_out, uint64_t dims_out[4]);
+
 /* textFile(arcs)/textFile(mapping) + mapToPair(split) + distinct + groupByKey + cache +
  * subtractByKey + distinct().count() (PageRank.java:26-60), then the device CSR build. */
 int pr_ingest_files(pr_ctx* ctx, const char* arcs_path, const char* mapping_path);

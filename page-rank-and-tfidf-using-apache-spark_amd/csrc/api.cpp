@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cmath>
@@ -50,6 +51,7 @@ struct pr_ctx {
   hipStream_t comm_stream = nullptr;
   std::vector<hipEvent_t> ev_chunk;
   hipEvent_t ev_rec = nullptr, ev_done = nullptr;
+  hipEvent_t ev_x0 = nullptr;     // chunk 0 of this round's x' (the hot prefix) has landed here
   int xchunks = 4;                // PR_XCHUNKS: row-launch chunks of the x' exchange
   int sx_checked = 0;             // sparse exchange: chunk count whose lists the ranks agreed on
   bool sx_ok = false;             //   (RCCL: count matrices compared once, all ranks alike)
@@ -61,6 +63,12 @@ struct pr_ctx {
   double ext_tol = 0.0;
   bool ext_tracked = false;
   prmi::IterState ext_hs{};
+  std::vector<hipEvent_t> ext_kev;  // SpMV event pairs of the externally exchanged rounds
+  // progress of the running (or last) round loop, readable from another thread (pr_progress):
+  // rounds whose work has been enqueued, and the event recorded behind each of them
+  std::atomic<int> prog_enq{0};
+  std::atomic<int> prog_done_hint{0};
+  std::vector<hipEvent_t> prog_ev;  // [PROG_EVENTS] ring: round t records prog_ev[(t-1) % PROG_EVENTS]
   // pr_run_static: this device's static scratch (resolved once in pr_create)
   prmi::StaticScratch scratch{};
 };
@@ -114,6 +122,19 @@ bool want_sx(const pr_ctx* c) {
   return c->opts.n_ranks > 1 && v != 0;
 }
 
+// Overlapped exchange (PR_XOVERLAP: 1 = on, the default; 0 = the round-2 schedule): the next
+// round's stream launch is cut in two.  Its first part -- every LDS phase and the L2-hot-range
+// tasks, almost all of its work -- reads only the hot prefix of each x slot, which travels as
+// chunk 0 of the exchange, so it starts as soon as that chunk has landed, while the other chunks,
+// the record all-gather and finalize are still under way; the cold-segment tasks and the row
+// launch (which needs the new addthis) follow once everything is in.  Needs the slice-major
+// layout with LDS blocks (p divides 8); off when a tolerance makes the host read every round.
+bool want_overlap(const pr_ctx* c, double tol) {
+  int v = 1;
+  if (const char* e = getenv("PR_XOVERLAP")) v = atoi(e);
+  return c->opts.n_ranks > 1 && v != 0 && tol == 0.0 && prmi::dev_can_split_stream(&c->dg);
+}
+
 // RCCL ranks: build the lists, then check once that every rank's receive counts equal its
 // peers' send counts (an all-gather of the count matrices); any mismatch anywhere turns the
 // sparse exchange off on every rank (a count mismatch inside a grouped send/recv would hang)
@@ -163,11 +184,32 @@ int sx_setup_rccl(pr_ctx* c, const std::vector<prmi::XChunk>& plan, bool& sx) {
   return PR_OK;
 }
 
+// Progress marks: one event per round behind the round's last enqueued work (a ring; the
+// watchdog thread of a caller only looks at recent rounds).  Created before the loop starts,
+// never resized while a loop runs.
+constexpr int PROG_EVENTS = 256;
+int ensure_progress(pr_ctx* c) {
+  while (static_cast<int>(c->prog_ev.size()) < PROG_EVENTS) {
+    hipEvent_t e;
+    HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->prog_ev.push_back(e);
+  }
+  c->prog_enq.store(0, std::memory_order_release);
+  c->prog_done_hint.store(0, std::memory_order_release);
+  return PR_OK;
+}
+int mark_progress(pr_ctx* c, int t, hipStream_t s) {
+  HIPCHK(c, hipEventRecord(c->prog_ev[(t - 1) % PROG_EVENTS], s));
+  c->prog_enq.store(t, std::memory_order_release);
+  return PR_OK;
+}
+
 // comm stream + events of the chunked exchange (created on first use)
 int ensure_xchg(pr_ctx* c) {
   if (!c->comm_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
   if (!c->ev_rec) HIPCHK(c, hipEventCreateWithFlags(&c->ev_rec, hipEventDisableTiming));
   if (!c->ev_done) HIPCHK(c, hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+  if (!c->ev_x0) HIPCHK(c, hipEventCreateWithFlags(&c->ev_x0, hipEventDisableTiming));
   if (const char* e = getenv("PR_XCHUNKS")) c->xchunks = std::max(1, atoi(e));
   return PR_OK;
 }
@@ -515,8 +557,11 @@ void pr_destroy(pr_ctx* c) {
     prmi::dev_free(&c->dg);
     for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_chunk) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->prog_ev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ext_kev) (void)hipEventDestroy(e);
     if (c->ev_rec) (void)hipEventDestroy(c->ev_rec);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    if (c->ev_x0) (void)hipEventDestroy(c->ev_x0);
     if (c->comm_stream) {
       (void)hipStreamSynchronize(c->comm_stream);
       (void)hipStreamDestroy(c->comm_stream);
@@ -602,6 +647,11 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
     return fail(c0, PR_E_EMPTY_DANGLING, "java.lang.UnsupportedOperationException: empty collection (iteration 1)");
   }
   const bool tracked = tol > 0.0 || (c0->opts.flags & PR_F_TRACK_RESIDUAL);
+  {
+    HIPCHK(c0, hipSetDevice(c0->device));
+    int rcp = ensure_progress(c0);
+    if (rcp) return rcp;
+  }
   auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < n; ++i) {
     HIPCHK(c0, hipSetDevice(ctxs[i]->device));
@@ -610,13 +660,18 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
   }
   int done = iterations;
   prmi::IterState hs{};
+  const bool ov = n > 1 && want_overlap(c0, tol);  // the schedule of pr_run, see want_overlap
+  // PR_XDELAY_US (measurements only): every chunk's copies start that late on the comm
+  // streams, standing in for a transfer time that device copies on one GPU do not have
+  int xdelay = 0;
+  if (const char* e = getenv("PR_XDELAY_US")) xdelay = std::max(0, atoi(e));
   std::vector<std::vector<prmi::XChunk>> plans(n);
   for (int i = 0; i < n; ++i) {
     pr_ctx* m = ctxs[i];
     HIPCHK(c0, hipSetDevice(m->device));
     int rc = ensure_xchg(m);
     if (rc) return fail(c0, rc, "exchange streams");
-    plans[i] = prmi::dev_exchange_plan(&m->dg, m->xchunks);
+    plans[i] = prmi::dev_exchange_plan(&m->dg, m->xchunks, ov);
     while (m->ev_chunk.size() < plans[i].size()) {
       hipEvent_t e;
       HIPCHK(c0, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -654,7 +709,17 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
     for (int i = 0; i < n; ++i) {
       pr_ctx* m = ctxs[i];
       HIPCHK(c0, hipSetDevice(m->device));
-      int rc = prmi::dev_round_stream(&m->dg, t, m->stream, nullptr);
+      int rc = PR_OK;
+      if (ov) {
+        if (t > 1) HIPCHK(c0, hipStreamWaitEvent(m->stream, m->ev_x0, 0));
+        rc = prmi::dev_round_stream(&m->dg, t, m->stream, nullptr, 1);
+        // (every member's ev_done: its copies out of this member's buffers have run too)
+        if (t > 1)
+          for (int q = 0; q < n; ++q) HIPCHK(c0, hipStreamWaitEvent(m->stream, ctxs[q]->ev_done, 0));
+        if (!rc) rc = prmi::dev_round_stream(&m->dg, t, m->stream, nullptr, 2);
+      } else {
+        rc = prmi::dev_round_stream(&m->dg, t, m->stream, nullptr, 0);
+      }
       for (size_t k = 0; !rc && k < plans[i].size(); ++k) {
         rc = prmi::dev_round_rows(&m->dg, t, mode, plans[i][k].b0, plans[i][k].b1, m->stream);
         if (!rc && sx) rc = prmi::dev_sx_pack(&m->dg, t, static_cast<int>(k), m->stream);
@@ -670,6 +735,12 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       DevGraph* dst = &mq->dg;
       HIPCHK(c0, hipSetDevice(mq->device));
       for (size_t k = 0; k < plans[q].size(); ++k) {
+        if (xdelay) {
+          for (int r = 0; r < n; ++r)
+            if (r != q) HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ctxs[r]->ev_chunk[k], 0));
+          int rcd = prmi::dev_delay_us(xdelay, mq->comm_stream);
+          if (rcd) return fail(c0, rcd, "delay kernel");
+        }
         for (int r = 0; r < n; ++r) {
           if (r == q) continue;
           DevGraph* src = &ctxs[r]->dg;
@@ -693,6 +764,7 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
           int rc = prmi::dev_sx_unpack(dst, t, static_cast<int>(k), mq->comm_stream);
           if (rc) return fail(c0, rc, "sparse exchange unpack");
         }
+        if (k == 0) HIPCHK(c0, hipEventRecord(mq->ev_x0, mq->comm_stream));
       }
       for (int r = 0; r < n; ++r) {
         DevGraph* src = &ctxs[r]->dg;
@@ -707,9 +779,15 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
     }
     // round t+1 starts once every member has its x' and a (and every copy out of this
     // member's slot has run, so the slot may be rewritten two rounds later)
-    for (int i = 0; i < n; ++i) {
-      HIPCHK(c0, hipSetDevice(ctxs[i]->device));
-      for (int q = 0; q < n; ++q) HIPCHK(c0, hipStreamWaitEvent(ctxs[i]->stream, ctxs[q]->ev_done, 0));
+    if (!ov || t == iterations)
+      for (int i = 0; i < n; ++i) {
+        HIPCHK(c0, hipSetDevice(ctxs[i]->device));
+        for (int q = 0; q < n; ++q) HIPCHK(c0, hipStreamWaitEvent(ctxs[i]->stream, ctxs[q]->ev_done, 0));
+      }
+    {
+      HIPCHK(c0, hipSetDevice(c0->device));
+      int rcp = mark_progress(c0, t, ov ? c0->comm_stream : c0->stream);
+      if (rcp) return rcp;
     }
     if (tol == 0.0) continue;
     HIPCHK(c0, hipMemcpyAsync(&hs, c0->dg.state, sizeof(hs), hipMemcpyDeviceToHost, c0->stream));
@@ -771,6 +849,14 @@ int pr_ext_begin(pr_ctx* c, int32_t iterations, double tol, uint64_t* bytes_per_
   c->ext_hs = prmi::IterState{};
   c->host_ranks_valid = false;
   c->last_iters = -1;
+  const int nk = std::min(iterations, 64);
+  while (static_cast<int>(c->ext_kev.size()) < 2 * nk) {
+    hipEvent_t e;
+    HIPCHK(c, hipEventCreate(&e));
+    c->ext_kev.push_back(e);
+  }
+  rc = ensure_progress(c);
+  if (rc) return rc;
   rc = prmi::dev_reset_state(g, c->stream);
   if (rc) return fail(c, rc, "reset state");
   if (bytes_per_rank) *bytes_per_rank = 8ull * g->maxA + 8ull * prmi::REC_WORDS;
@@ -785,7 +871,9 @@ int pr_ext_round(pr_ctx* c, int32_t t, void* send) {
     return fail(c, PR_E_ARG, "pr_ext_round: call pr_ext_begin, then rounds 1, 2, ... in order");
   DevGraph* g = &c->dg;
   const int mode = c->ext_tracked ? 2 : (t == c->ext_iters ? 1 : 0);
-  rc = prmi::dev_round_compute(g, t, mode, c->stream, nullptr, nullptr);
+  const bool timed = 2 * t <= static_cast<int>(c->ext_kev.size());
+  rc = prmi::dev_round_compute(g, t, mode, c->stream, timed ? c->ext_kev[2 * (t - 1)] : nullptr,
+                               timed ? c->ext_kev[2 * (t - 1) + 1] : nullptr);
   if (rc) return fail(c, rc, "round compute");
   // this rank's slot of x' and its exact record, in that order
   char* out = static_cast<char*>(send);
@@ -817,6 +905,8 @@ int pr_ext_complete(pr_ctx* c, int32_t t, const void* recv_all, int32_t* stop) {
   HIPCHK(c, hipMemcpyAsync(&c->ext_hs, g->state, sizeof(c->ext_hs), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->ext_done = t;
+  c->prog_enq.store(t, std::memory_order_release);       // (the stream was synchronized above)
+  c->prog_done_hint.store(t, std::memory_order_release);
   const bool conv = c->ext_tol > 0.0 && c->ext_hs.resid <= c->ext_tol;
   if (stop) *stop = conv ? 1 : 0;
   // the reduce of a round (PageRank.java:125) saw an empty danglingMap: the job dies there
@@ -837,6 +927,18 @@ int pr_ext_end(pr_ctx* c, pr_stats* st) {
   s.nnz = c->dg.nnz;
   s.n_vertices = c->dg.n;
   s.iterations = c->ext_done;
+  {  // average SpMV time of the rounds that carried events (the first 64)
+    double kms = 0.0;
+    int nm = 0;
+    for (int t = 0; t < c->ext_done && 2 * t + 1 < static_cast<int>(c->ext_kev.size()); ++t) {
+      float k = 0.f;
+      if (hipEventElapsedTime(&k, c->ext_kev[2 * t], c->ext_kev[2 * t + 1]) == hipSuccess) {
+        kms += k;
+        ++nm;
+      }
+    }
+    s.ms_spmv_kernel = nm ? kms / nm : 0.0;
+  }
   s.residual = c->ext_tracked ? c->ext_hs.resid : 0.0;
   s.rank_sum = c->ext_tracked ? c->ext_hs.rank_sum : 0.0;
   c->last_iters = c->ext_done;
@@ -1023,7 +1125,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   }
   const bool tracked = tol > 0.0 || (c->opts.flags & PR_F_TRACK_RESIDUAL);
   const int nk = std::min(iterations, 64);
-  while (static_cast<int>(c->kev.size()) < 2 * nk) {
+  while (static_cast<int>(c->kev.size()) < 4 * nk) {  // per round: [A0, A1, B0, B1]
     hipEvent_t e;
     HIPCHK(c, hipEventCreate(&e));
     c->kev.push_back(e);
@@ -1033,10 +1135,11 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   const int p = c->opts.n_ranks;
   std::vector<prmi::XChunk> plan;
   bool sx = false;  // sparse x' exchange this run
+  const bool ov = want_overlap(c, tol);
   if (p > 1) {  // (before ev_start: list building and its collectives are set-up, not rounds)
     rc = ensure_xchg(c);
     if (rc) return rc;
-    plan = prmi::dev_exchange_plan(g, c->xchunks);
+    plan = prmi::dev_exchange_plan(g, c->xchunks, ov);
     while (c->ev_chunk.size() < plan.size()) {
       hipEvent_t e;
       HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1047,14 +1150,18 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       if (rc) return rc;
     }
   }
+  rc = ensure_progress(c);
+  if (rc) return rc;
   rc = prmi::dev_reset_state(g, c->stream);
   if (rc) return fail(c, rc, "reset state");
   HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
   for (int t = 1; t <= iterations; ++t) {
     const int mode = tracked ? 2 : (t == iterations ? 1 : 0);
     prmi::Span round("prmi:round");
-    hipEvent_t e0 = t <= nk ? c->kev[2 * (t - 1)] : nullptr;
-    hipEvent_t e1 = t <= nk ? c->kev[2 * (t - 1) + 1] : nullptr;
+    hipEvent_t e0 = t <= nk ? c->kev[4 * (t - 1)] : nullptr;      // stream launch (part 1)
+    hipEvent_t eA1 = t <= nk ? c->kev[4 * (t - 1) + 1] : nullptr;  // overlapped: end of part 1
+    hipEvent_t eB0 = t <= nk ? c->kev[4 * (t - 1) + 2] : nullptr;  //   and start of part 2
+    hipEvent_t e1 = t <= nk ? c->kev[4 * (t - 1) + 3] : nullptr;   // end of the row launch
     if (p == 1) {
       rc = prmi::dev_round_single(g, t, mode, tracked, c->stream, e0, e1);
       if (rc) return fail(c, rc, "round");
@@ -1066,7 +1173,18 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       // records are all-gathered after the last rows, finalize runs on the comm stream, and
       // the next round's stream launch waits for it.
       double* xf = prmi::dev_x_out(g, t);
-      rc = prmi::dev_round_stream(g, t, c->stream, e0);
+      if (ov) {
+        // part 1 needs chunk 0 of the last round only; part 2 and the rows need the rest of
+        // x', and the rows the new addthis (both behind ev_done on the comm stream)
+        if (t > 1) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_x0, 0));
+        rc = prmi::dev_round_stream(g, t, c->stream, e0, 1);
+        if (rc) return fail(c, rc, "round compute");
+        if (eA1) HIPCHK(c, hipEventRecord(eA1, c->stream));
+        if (t > 1) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
+        rc = prmi::dev_round_stream(g, t, c->stream, eB0, 2);
+      } else {
+        rc = prmi::dev_round_stream(g, t, c->stream, e0, 0);
+      }
       if (rc) return fail(c, rc, "round compute");
       for (size_t k = 0; k < plan.size(); ++k) {
         rc = prmi::dev_round_rows(g, t, mode, plan[k].b0, plan[k].b1, c->stream);
@@ -1102,14 +1220,18 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
           rc = prmi::dev_sx_unpack(g, t, static_cast<int>(k), c->comm_stream);
           if (rc) return fail(c, rc, "sparse exchange unpack");
         }
+        if (k == 0) HIPCHK(c, hipEventRecord(c->ev_x0, c->comm_stream));  // the hot prefix is in
       }
       HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_rec, 0));
       NCCLCHK(c, ncclAllGather(g->rec_local, g->rec_all, prmi::REC_WORDS, ncclUint64, c->comm, c->comm_stream));
       rc = prmi::dev_round_finalize(g, t, tracked, c->comm_stream);
       if (rc) return fail(c, rc, "round finalize");
       HIPCHK(c, hipEventRecord(c->ev_done, c->comm_stream));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));  // round t+1 needs x' and a
+      // round t+1 needs x' and a: all of it at once, or (overlapped) in the two steps above
+      if (!ov || t == iterations) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
     }
+    rc = mark_progress(c, t, p > 1 ? c->comm_stream : c->stream);
+    if (rc) return rc;
     if (tol > 0.0) {
       HIPCHK(c, hipMemcpyAsync(&hs, g->state, sizeof(hs), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1127,8 +1249,14 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   double kms = 0.0;
   const int nmeas = std::min(done, nk);
   for (int t = 0; t < nmeas; ++t) {
-    float k = 0.f;
-    if (hipEventElapsedTime(&k, c->kev[2 * t], c->kev[2 * t + 1]) == hipSuccess) kms += k;
+    float k = 0.f, k2 = 0.f;
+    if (p > 1 && ov) {  // the two parts of the round's SpMV, without the wait between them
+      if (hipEventElapsedTime(&k, c->kev[4 * t], c->kev[4 * t + 1]) == hipSuccess &&
+          hipEventElapsedTime(&k2, c->kev[4 * t + 2], c->kev[4 * t + 3]) == hipSuccess)
+        kms += k + k2;
+    } else if (hipEventElapsedTime(&k, c->kev[4 * t], c->kev[4 * t + 3]) == hipSuccess) {
+      kms += k;
+    }
   }
   s.iterations = done;
   s.ms_total = ms;
@@ -1138,7 +1266,8 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   s.residual = tracked ? hs.resid : 0.0;
   s.rank_sum = tracked ? hs.rank_sum : 0.0;
   // the reduce of round err_iter saw an empty danglingMap: the reference dies there
-  if (hs.err_iter != 0 && hs.err_iter <= done) {
+  // (not under the timing-only row filters, whose ranks are wrong by construction)
+  if (hs.err_iter != 0 && hs.err_iter <= done && !g->tune.dropdeg && !g->tune.keepdeg) {
     s.failed_iteration = t0 + hs.err_iter;
     if (st) *st = s;
     return fail(c, PR_E_EMPTY_DANGLING,
@@ -1243,6 +1372,65 @@ int pr_run_static(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   }
   c->last_iters = done;
   if (st) *st = s;
+  return PR_OK;
+}
+
+// Diagnostics of the running (or last) round loop; callable from another thread while the
+// loop's entry point blocks (it reads two atomics and queries events, nothing else).
+int pr_progress(pr_ctx* c, int32_t* rounds_enqueued, int32_t* rounds_done) {
+  if (!c) return PR_E_ARG;
+  const int enq = c->prog_enq.load(std::memory_order_acquire);
+  int done = std::min(c->prog_done_hint.load(std::memory_order_acquire), enq);
+  if (c->has_device && static_cast<int>(c->prog_ev.size()) == PROG_EVENTS) {
+    // rounds complete in order: advance past every recent round whose event has fired
+    done = std::max(done, enq - PROG_EVENTS);
+    while (done < enq && hipEventQuery(c->prog_ev[done % PROG_EVENTS]) == hipSuccess) ++done;
+    c->prog_done_hint.store(done, std::memory_order_release);
+  }
+  if (rounds_enqueued) *rounds_enqueued = enq;
+  if (rounds_done) *rounds_done = done;
+  return PR_OK;
+}
+
+int pr_layout_map(int32_t n_ranks, int32_t rank, uint32_t n_a, uint32_t n_b, uint32_t n_c,
+                  uint64_t count, const uint32_t* internal_ids, uint32_t* owner_out,
+                  uint32_t* local_row_out, uint64_t* x_pos_out, uint64_t dims_out[4]) {
+  if (count && !internal_ids) return PR_E_ARG;
+  return prmi::host_layout_map(n_ranks, rank, n_a, n_b, n_c, count, internal_ids, owner_out,
+                               local_row_out, x_pos_out, dims_out);
+}
+
+int pr_selftest_sum_order(pr_ctx* c, uint32_t cases, uint32_t launches, uint64_t* copies,
+                          uint64_t* differing, uint64_t* lane_order_cases) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  if (!copies || !differing || !lane_order_cases || cases == 0 || launches == 0)
+    return fail(c, PR_E_ARG, "pr_selftest_sum_order: null output or empty test");
+  std::string e;
+  rc = prmi::dev_selftest_lds_order(cases, launches, c->stream, copies, differing, lane_order_cases, &e);
+  if (rc) return fail(c, rc, "self-test: " + e);
+  return PR_OK;
+}
+
+int pr_comm_query(pr_ctx* c, int32_t* transport, int32_t* comm_ranks, int32_t* comm_rank) {
+  if (!c) return PR_E_ARG;
+  int tr = 0, n = 1, r = 0;
+  if (c->comm) {
+    tr = 1;
+    NCCLCHK(c, ncclCommCount(c->comm, &n));
+    NCCLCHK(c, ncclCommUserRank(c->comm, &r));
+  } else if (!c->group.empty()) {
+    tr = 2;
+    n = static_cast<int>(c->group.size());
+    r = c->opts.rank;
+  } else if (c->external) {
+    tr = 3;
+    n = c->opts.n_ranks;
+    r = c->opts.rank;
+  }
+  if (transport) *transport = tr;
+  if (comm_ranks) *comm_ranks = n;
+  if (comm_rank) *comm_rank = r;
   return PR_OK;
 }
 

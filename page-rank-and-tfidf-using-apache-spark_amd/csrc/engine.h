@@ -80,8 +80,9 @@ struct Tuning {
   uint32_t rb_heavy = 256;  // PR_RBH: rows per heavy row-launch block
   uint32_t rxg = 16;     // PR_RXG: consecutive row-launch blocks per XCD (1 = round-robin)
   uint32_t heavy_deg = 128; // PR_HDEG: rows with in-degree >= this get heavy blocks (0 = none)
-  int nlds = 20;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill; 18
-                        // before the workgroup task claims, 20 with them: +2 %, interleaved runs)
+  int nlds = 20;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill).  Unset,
+                        // the build sizes it to the graph: the hottest ~11.5 % of a slice's
+                        // class-A columns (20 blocks at R-MAT scale 26 on one rank)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
   // PR_NT: 2 = non-temporal piece stores (they stop evicting x from the L2s: +3 %), 0 =
   // regular stores.  Non-temporal stream loads and LDS fills were measured slower.
@@ -97,6 +98,8 @@ struct Tuning {
   uint32_t dpull = 0;   // PR_DPULL: direct-pull experiment for rows below this in-degree
                         // (timing only, single rank; engine.hip spmv_dpull)
   uint32_t dropdeg = 0; // PR_DROPDEG: rows below this in-degree leave the streams (timing only)
+  uint32_t keepdeg = 0; // PR_KEEPDEG: rows at or above this in-degree leave the streams (timing only)
+  int stream_cus = 32;  // PR_STREAM_CUS: stream workgroups (= compute units) per XCD
   int l2late = 0;       // PR_L2LATE: L2-role waves prefetch the next task's columns after
                         // their gathers instead of before (see StreamArgs::l2late)
   int lean = 1;         // PR_LEAN: 1 = the lean per-task instruction stream of the stream launch
@@ -190,6 +193,9 @@ struct DevGraph {
   double* sx_rbuf = nullptr;      // [recvs]
   std::vector<uint64_t> sx_so, sx_ro;  // [chunks * p + 1] offsets of each (chunk, peer) list
   int sx_chunks = 0;              // chunk count the lists were built for (0 = none)
+  uint64_t sx_plan_sig = 0;       // and a hash of that plan's pieces
+  uint32_t l2split[NSLICE] = {0}; // first L2-group task of each slice that needs x behind the
+                                  // hot prefix (the two-part stream launch of p > 1)
   IterState* state = nullptr;
   // row launch: blocks of 1024 rows (class A, then class B), streams = slices x segments
   uint32_t nb_rows = 0, nb_rows_a = 0, n_streams = 0;
@@ -247,7 +253,13 @@ int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev
                       hipEvent_t ev1);
 // The same in three steps (the row launch may be cut into block ranges [b0, b1), e.g. for the
 // chunked exchange): the stream launch; rows of blocks [b0, b1); the record reduction.
-int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0);
+// part 0: the whole stream launch.  Parts 1 and 2 cut it for the overlapped exchange (p > 1,
+// dev_can_split_stream): part 1 = the first LDS phases + the L2-hot-range tasks, which read
+// only the hot prefix of each x slot sub-region (chunk 0 of a hot-first exchange plan) and the
+// constant class-C entries; part 2 = the other LDS phases + the cold-segment tasks, which read
+// the rest as well.
+int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0, int part = 0);
+bool dev_can_split_stream(const DevGraph* g);
 int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipStream_t s);
 int dev_round_reduce(DevGraph* g, hipStream_t s, hipEvent_t ev1);
 // p = 1: the whole round (stream, rows, then record reduction + finalize in one launch).
@@ -262,7 +274,8 @@ struct XChunk {
   uint32_t b0 = 0, b1 = 0;
   std::vector<XPiece> pieces;
 };
-std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K);
+// hot_first: chunk 0 = the hot prefix (LDS blocks + L2-hot range) of every slot sub-region
+std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K, bool hot_first = false);
 // Sparse exchange: build the per-(chunk, peer) pack / unpack lists for `plan` (once per chunk
 // count); pack chunk k of this rank's slot of x'(t) into sx_sbuf; unpack chunk k's received
 // entries from sx_rbuf into x'(t).  Lists are in (chunk, peer, piece, entry) order on every
@@ -321,6 +334,22 @@ constexpr int INGEST_NOFIT = 100;
 int dev_ingest_text(const char* arcs, size_t alen, const char* map, size_t mlen, HostGraph* g,
                     ParseError* pe, hipStream_t s, std::string* err);
 int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s, std::string* err);
+// Self-test of the order in which one ds_add_f64 instruction applies its lanes' same-address
+// adds (the row launch's sums rest on it): `cases` lane/address/value patterns, each launched
+// `launches` times on a grid covering every CU.  copies = accumulator sets compared, differing =
+// those that differ from the first copy of their case, lane_order_cases = cases whose bits
+// equal the ascending-lane serial sum.
+// The kernels' layout functions on the host: for cnt internal vertex ids k (rows: k < nA + nB;
+// columns: class A k < nA, class C nA + nB <= k < nA + nB + nC) the owner rank and local row of
+// each row (0xFFFFFFFF for non-rows) and the x position of each column (~0 for non-columns), as
+// rank `rank` of p sees them; dims = {slot length maxA, x length, local rows, local class-A rows}.
+int host_layout_map(int p, int rank, uint32_t nA, uint32_t nB, uint32_t nC, uint64_t cnt,
+                    const uint32_t* k, uint32_t* owner, uint32_t* local, uint64_t* xp,
+                    uint64_t dims[4]);
+// A one-wave kernel that sleeps ~us microseconds on stream s (exchange measurements only).
+int dev_delay_us(int us, hipStream_t s);
+int dev_selftest_lds_order(uint32_t cases, uint32_t launches, hipStream_t s, uint64_t* copies,
+                           uint64_t* differing, uint64_t* lane_order_cases, std::string* err);
 // Internal id of this rank's local row l (host copy of the device mapping).
 inline uint32_t row_internal(const DevGraph* g, uint32_t l) {
   return (((l / CHUNK) * static_cast<uint32_t>(g->p) + static_cast<uint32_t>(g->rank)) * CHUNK) +

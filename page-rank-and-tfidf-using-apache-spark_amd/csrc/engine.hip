@@ -44,7 +44,7 @@ namespace prmi {
 // =======================================================================================
 // device helpers
 // =======================================================================================
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+__device__ __host__ __forceinline__ uint64_t mix64(uint64_t x) {
   x ^= x >> 30;
   x *= 0xBF58476D1CE4E5B9ull;
   x ^= x >> 27;
@@ -408,6 +408,12 @@ struct StreamArgs {
                              // L2 tasks are shared out over the LDS phases, see l2mode)
   uint32_t wgdyn;            // PR_WGDYN: LDS waves claim their workgroup's tasks from an LDS
                              // counter (1) or take them round-robin (0)
+  uint32_t l2lo[NSLICE];     // L2-group tasks [l2lo, l2hi) of each slice this launch sweeps
+  uint32_t l2hi[NSLICE];
+  uint32_t ph_lo, ph_hi;     // LDS phases [ph_lo, ph_hi) this launch runs (all of them unless
+                             // the launch is one part of a cut launch)
+  uint32_t part;             // 2 with ph_lo == ph_hi: no LDS phase at all, every wave sweeps
+                             // the L2 tasks above; otherwise informational
   uint32_t l2late;           // PR_L2LATE: the L2-role waves issue the next task's column loads
                              // after their sixteen gathers have landed instead of before them
                              // (vmcnt counts in order: gathers issued behind the prefetch wait
@@ -587,7 +593,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // (gathers through the XCD's L2) for the whole launch while the other LW waves run the LDS
   // phases: latency-bound gathers beside bandwidth-bound LDS tasks.  The LW waves then sync
   // with an LDS-counter barrier of their own (the L2 waves never wait).
-  const bool split = SPLIT && A.l2w != 0u && A.nlds != 0u;
+  const bool onlyl2 = A.part == 2u && A.ph_lo >= A.ph_hi;
+  const bool split = SPLIT && A.l2w != 0u && A.nlds != 0u && !onlyl2;
   const uint32_t LW = split ? wpb - A.l2w : wpb;
   const bool l2role = split && wv >= LW;
   const uint32_t rw = l2role ? A.l2w : LW;  // waves per workgroup in this wave's role
@@ -637,7 +644,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   u32x4 cn[4];
   uint32_t bnx = 0, tpn = 0;
   const uint32_t l2g = j * ngs + A.nlds;
-  const uint32_t l2b = A.gtask[l2g], l2e = A.gtask[l2g + 1];
+  const uint32_t l2g0 = A.gtask[l2g];              // first task of the slice's L2 group
+  const uint32_t l2b = A.l2lo[j], l2e = A.l2hi[j];  // the part of it this launch sweeps
   const uint64_t l2base = A.gbase[l2g];
   auto fetch = [&](uint32_t tt, bool lds_task, uint32_t gtb, uint64_t gbs) {
     // PR_DBG=2048 / 4096 (timing only, wrong sums): every LDS-group / L2-group task reads the
@@ -673,12 +681,13 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // with 1/nlds of the L2 part's tasks (LDS-bound and L2-bound work side by side); with no
   // LDS blocks the single phase is the whole stream.
   const bool l2last = A.l2mode == 1u && A.nlds && !split;  // one final phase for every L2 task
-  const uint32_t nph = A.nlds ? A.nlds + ((l2last || split) ? 1u : 0u) : 1u;  // (stamp slots)
-  const uint32_t g0 = l2role ? A.nlds : 0u, g1 = split ? (l2role ? A.nlds + 1u : A.nlds) : nph;
+  const uint32_t nph = (A.nlds && !onlyl2) ? A.nlds + ((l2last || split) ? 1u : 0u) : 1u;  // (stamp slots)
+  const uint32_t g0 = l2role ? A.nlds : (split ? A.ph_lo : 0u),
+                 g1 = split ? (l2role ? A.nlds + 1u : A.ph_hi) : nph;
   for (uint32_t gi = g0; gi < g1; ++gi) {
     uint32_t tb = l2b, te = l2b, rb = l2b, re = l2e;  // LDS-block tasks, L2 share
     uint64_t lbase = 0;
-    if (gi == A.nlds && (l2last || l2role)) {
+    if (onlyl2 || (gi == A.nlds && (l2last || l2role))) {
       // the L2 phase / role: no LDS block, the whole L2 group (segments swept in order)
     } else if (A.nlds) {
       tb = A.gtask[j * ngs + gi];
@@ -717,7 +726,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     };
     auto fetch_u = [&](uint32_t u) {
       const bool lt = is_lds(u);
-      fetch(task_of(u), lt, lt ? tb : l2b, lt ? lbase : l2base);
+      fetch(task_of(u), lt, lt ? tb : l2g0, lt ? lbase : l2base);
     };
     const uint32_t nu = nL + nR;
     auto claim = [&]() -> uint32_t {
@@ -788,6 +797,16 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     const int C = LEAN ? wave_incl_scan_lean(cnt) : wave_incl_scan(cnt, lane);
     const uint32_t first = static_cast<uint32_t>(C - cnt);  // task-relative index of the lane's first start
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(C, 63));  // pieces of the task
+    // PR_DBG=8192 (timing only, wrong sums): a task made almost only of single-edge pieces
+    // stores its sixteen gathered values per lane as if lane l's edge k were piece 64 k + l --
+    // the store pattern of a column-major all-singles task: no sums, no scan, no staging
+    const bool fastd = (A.dbg & 8192u) != 0u && total >= 768u;
+    if (fastd) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k)
+        if (64u * k + static_cast<uint32_t>(lane) < total)
+          __builtin_nontemporal_store(v[k], part + tp0 + 64u * k + lane);
+    } else {
     // one pass over the lane's edges: pv[k] = the running sum just before edge k (for a start
     // bit k that is the piece closing before k; for the lane's first start it is the head,
     // the edges before it), run = the open piece at the lane's end.  Same adds, same order as
@@ -874,6 +893,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    }  // !fastd
       // PR_L2LATE=2 (A/B): the L2-role waves wait for their piece stores right here; the cost
       // bounds what the gathers' in-order wait can lose to stores still in flight
       if (l2role && A.l2late == 2u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -882,6 +902,53 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     }
     if (stp && lane == 0) stp[1 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+// ---- self-test of the row launch's summation order ---------------------------------------
+// The row launch adds pieces into LDS accumulators with one ds_add_f64 per lane per line; lanes
+// of one instruction that hit the same row collide, and the sums are only reproducible if the
+// hardware applies such same-address adds in an order that depends on nothing but the lanes
+// and addresses.  k_lds_order issues exactly that instruction form -- 64 lanes, one atomicAdd,
+// addresses drawn from M rows, values whose exponents differ so that every order rounds
+// differently -- from every wave of a large grid and stores the accumulators' bits; the host
+// compares all copies (dev_selftest_lds_order).
+__device__ __host__ __forceinline__ uint64_t st_mix(uint64_t c, uint64_t l) {
+  uint64_t x = (c + 1) * 0x9E3779B97F4A7C15ull + l * 0xD1B54A32D192ED03ull;
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+constexpr int ST_ROWS = 8;  // accumulator rows of a case (M = 1 + case % 8 of them are hit)
+__device__ __host__ __forceinline__ void st_case(uint32_t c, uint32_t lane, uint32_t* row, double* val) {
+  const uint64_t h = st_mix(c, lane);
+  const uint32_t M = 1u + c % ST_ROWS;
+  *row = static_cast<uint32_t>(h % M);
+  // 1.m x 2^-e, e in [0, 40): sums of such values round differently in different orders
+  const uint64_t mant = (h >> 12) & ((1ull << 52) - 1);
+  const uint64_t e = 1023ull - (h >> 3) % 40ull;
+  const uint64_t bits = (e << 52) | mant;
+#ifdef __HIP_DEVICE_COMPILE__
+  *val = __longlong_as_double(static_cast<long long>(bits));
+#else
+  memcpy(val, &bits, 8);
+#endif
+}
+__global__ __launch_bounds__(BLOCK) void k_lds_order(uint32_t c, uint64_t* out) {
+  __shared__ double acc[BLOCK / 64][ST_ROWS];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < ST_ROWS) acc[wv][lane] = 0.0;
+  __syncthreads();
+  uint32_t row;
+  double val;
+  st_case(c, lane, &row, &val);
+  atomicAdd(&acc[wv][row], val);  // one ds_add_f64 over the 64 lanes, as spmv_rows issues them
+  __syncthreads();
+  if (lane < ST_ROWS)
+    out[(static_cast<uint64_t>(blockIdx.x) * (BLOCK / 64) + wv) * ST_ROWS + lane] =
+        static_cast<uint64_t>(__double_as_longlong(acc[wv][lane]));
 }
 
 // Sum the NSHARD shards into one record and clear them for the next round (one 256-thread
@@ -1144,7 +1211,7 @@ __device__ __host__ __forceinline__ uint32_t row_of(const Layout& L, uint32_t l)
 // inside it in the sub-region of their slice (chunk c = k>>4 has slice c&7 and, as p
 // divides 8, owner c%p = (c&7)%p), chunks of a slice in order -- each XCD's slice is one
 // contiguous, hotness-ordered address range (all L2 sets and channels in use).
-__device__ __forceinline__ uint32_t xpos(const Layout& L, uint32_t k) {
+__device__ __host__ __forceinline__ uint32_t xpos(const Layout& L, uint32_t k) {
   if (k < L.nA) {
     if (!L.sm) return owner_of(L, k) * L.maxA + local_of(L, k);
     const uint32_t c = k / CHUNK, sl = chunk_slice(c, L.snake);
@@ -1279,15 +1346,19 @@ struct NotDropped {
 };
 __global__ void k_stream_keys(const uint64_t* uk, uint64_t nnz, int nb, const uint32_t* inv,
                               Layout L, StreamGeo G, uint64_t* out, const uint32_t* indeg,
-                              uint32_t dropdeg) {
+                              uint32_t dropdeg, uint32_t keepdeg) {
   PRMI_BLOCK_LOOP(nnz) {
     const uint64_t e = blk_ * blockDim.x + threadIdx.x;
     if (e >= nnz) continue;
     const uint64_t k = uk[e];
     // PR_DROPDEG (timing only, wrong ranks): rows below this in-degree leave the streams
-    if (dropdeg && indeg[static_cast<uint32_t>(k >> nb)] < dropdeg) {
-      out[e] = DROP_KEY;
-      continue;
+    // (PR_KEEPDEG: rows at or above that in-degree leave instead)
+    if (dropdeg || keepdeg) {
+      const uint32_t di = indeg[static_cast<uint32_t>(k >> nb)];
+      if (di < dropdeg || (keepdeg && di >= keepdeg)) {
+        out[e] = DROP_KEY;
+        continue;
+      }
     }
     const uint32_t kd = inv[static_cast<uint32_t>(k >> nb)];
     const uint32_t ks = inv[static_cast<uint32_t>(k & ((1ull << nb) - 1))];
@@ -1341,6 +1412,21 @@ __global__ void k_group_starts(const uint64_t* key, uint64_t n, StreamGeo G,
     if (e == 0 || group_of_key(G, key[e - 1]) != gr)
       atomicMin(&starts[gr], static_cast<unsigned long long>(e));
   }
+}
+
+// first sorted edge of slice j whose segment lies behind the L2-hot range (one thread per slice,
+// lower bound over the sorted stream keys)
+__global__ void k_cold_start(const uint64_t* key, uint64_t n, StreamGeo G, uint64_t* idx) {
+  const uint32_t j = threadIdx.x;
+  if (j >= NSLICE) return;
+  const uint64_t want = (static_cast<uint64_t>(j) << (G.sgb + G.rb + G.qb)) |
+                        (static_cast<uint64_t>(G.nlds + 1u) << (G.rb + G.qb));
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    if (key[mid] < want) lo = mid + 1; else hi = mid;
+  }
+  idx[j] = lo;
 }
 
 // column of every stream edge (LDS groups: u16 offset inside the block; L2 group: x position)
@@ -1895,6 +1981,36 @@ uint32_t owned_rows(uint32_t cnt, uint32_t p, uint32_t j) {
   return r;
 }
 
+// The row deal and x layout of rank `rank` of `p` for a graph with nA / nB / nC vertices in
+// classes A / B / C: everything dev_build and the exchange derive from the class counts.
+struct LayoutDims {
+  Layout L;
+  uint64_t X;            // x length
+  uint32_t lrows, lA;    // local rows, local class-A rows
+};
+LayoutDims make_layout(int p, int rank, uint32_t nA, uint32_t nB, uint32_t nC) {
+  LayoutDims d{};
+  const uint32_t P = static_cast<uint32_t>(p), RK = static_cast<uint32_t>(rank);
+  const bool sm = (NSLICE % P) == 0 && env_int("PR_SLICE_MAJOR", 1) != 0;
+  const bool snake = sm && P == 1 && env_int("PR_SNAKE", 1) != 0;
+  uint32_t SL = 0, SLC = 0, maxA = 0;
+  if (sm) {
+    const uint32_t chA = (nA + CHUNK - 1) / CHUNK, chC = (nC + CHUNK - 1) / CHUNK;
+    SL = CHUNK * ((chA + NSLICE - 1) / NSLICE);
+    SLC = CHUNK * ((chC + NSLICE - 1) / NSLICE);
+    maxA = (NSLICE / P) * SL;
+    d.X = static_cast<uint64_t>(P) * maxA + static_cast<uint64_t>(NSLICE) * SLC;
+  } else {
+    for (uint32_t j = 0; j < P; ++j) maxA = std::max(maxA, owned_rows(nA, P, j));
+    maxA = (maxA + CHUNK - 1) / CHUNK * CHUNK;
+    d.X = static_cast<uint64_t>(P) * maxA + nC;
+  }
+  d.L = Layout{P, RK, nA, nA + nB, nC, maxA, sm ? 1u : 0u, SL, SLC, snake ? 1u : 0u};
+  d.lrows = owned_rows(nA + nB, P, RK);
+  d.lA = owned_rows(nA, P, RK);
+  return d;
+}
+
 
 }  // namespace
 
@@ -1919,15 +2035,18 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   // a rank's share of each (slice, LDS block) phase shrinks with p while the per-phase cost
   // (block fill, phase tail) stays: fewer blocks per slice at p > 1 (measured per-rank SpMV
   // at scale 26: p = 2 best at 15, p = 4 and 8 at 12; profiles/r01/multirank/)
-  const int nlds_def = p >= 4 ? 12 : (p >= 2 ? 15 : T.nlds);
-  T.nlds = std::max(0, std::min(64, env_int("PR_NLDS", nlds_def)));
+  // PR_NLDS overrides; otherwise the count follows the graph (below, once the slice length is
+  // known)
+  const int nlds_env = env_int("PR_NLDS", -1);
   T.stream_wg = std::max(1, std::min(2, env_int("PR_STREAM_WG", T.stream_wg)));
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));
   T.l2mode = env_int("PR_L2MODE", T.l2mode);
   T.l2w = std::max(0, std::min(12, env_int("PR_L2W", T.l2w)));
   T.l2late = env_int("PR_L2LATE", T.l2late);
+  T.stream_cus = env_int("PR_STREAM_CUS", T.stream_cus);
   T.dpull = static_cast<uint32_t>(std::max(0, env_int("PR_DPULL", 0)));
   T.dropdeg = static_cast<uint32_t>(std::max(0, env_int("PR_DROPDEG", 0)));
+  T.keepdeg = static_cast<uint32_t>(std::max(0, env_int("PR_KEEPDEG", 0)));
   const uint32_t n = in.n;
   const uint64_t m = in.m;
   g->n = n;
@@ -2087,23 +2206,17 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   g->nC = start[3] - start[2];
   g->nD = start[4] - start[3];
   g->R = g->nA + g->nB;
-  const uint32_t P = static_cast<uint32_t>(p), RK = static_cast<uint32_t>(rank);
-  g->sm = (NSLICE % P) == 0 && env_int("PR_SLICE_MAJOR", 1) != 0;
-  g->snake = g->sm && P == 1 && env_int("PR_SNAKE", 1) != 0;
-  if (g->sm) {
-    const uint32_t chA = (g->nA + CHUNK - 1) / CHUNK, chC = (g->nC + CHUNK - 1) / CHUNK;
-    g->SL = CHUNK * ((chA + NSLICE - 1) / NSLICE);
-    g->SLC = CHUNK * ((chC + NSLICE - 1) / NSLICE);
-    g->maxA = (NSLICE / P) * g->SL;
-    g->X = static_cast<uint64_t>(P) * g->maxA + static_cast<uint64_t>(NSLICE) * g->SLC;
-  } else {
-    uint32_t maxA = 0;
-    for (uint32_t j = 0; j < P; ++j) maxA = std::max(maxA, owned_rows(g->nA, P, j));
-    g->maxA = (maxA + CHUNK - 1) / CHUNK * CHUNK;
-    g->X = static_cast<uint64_t>(P) * g->maxA + g->nC;
+  {
+    const LayoutDims d = make_layout(p, rank, g->nA, g->nB, g->nC);
+    g->sm = d.L.sm != 0;
+    g->snake = d.L.snake != 0;
+    g->SL = d.L.SL;
+    g->SLC = d.L.SLC;
+    g->maxA = d.L.maxA;
+    g->X = d.X;
+    g->lrows = d.lrows;
+    g->lA = d.lA;
   }
-  g->lrows = owned_rows(g->R, P, RK);
-  g->lA = owned_rows(g->nA, P, RK);
   const Layout L = layout_of(g);
 
   span.next("prmi:build:x vectors + row data");
@@ -2139,6 +2252,20 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     G.nlds = 0;
     if (g->sm && g->X < (1ull << 28) && T.hot_lds > 0) {
       G.H = std::min<uint32_t>(HOT_MAX, T.hot_lds) & ~1u;  // even: 16-byte LDS-DMA fills
+      // LDS blocks per slice: the measured optimum covers the hottest ~11.5 % of a slice's
+      // class-A columns whatever the size of the graph (R-MAT scale 22 / 24 / 26 / 28 on one
+      // rank: 2 / 6 / 20 / 64 blocks; a fixed 20 cost 33 % at scale 22 and 22 % at scale 28),
+      // and a rank of p >= 2 takes 0.75 x (p = 2) or 0.6 x (p >= 4) of that: its share of every
+      // phase shrinks with p while the per-phase cost stays (scale 26: 15 and 12; scale 28 at
+      // 8 ranks: 40 against 24 and 12).  Cold segments widen until the row launch's stream
+      // table holds every (slice, segment).
+      int want = nlds_env;
+      if (want < 0) {
+        const double f = p >= 4 ? 0.6 : (p >= 2 ? 0.75 : 1.0);
+        want = static_cast<int>(0.115 * f * static_cast<double>(g->SL) / G.H + 0.5);
+        want = std::max(1, want);
+      }
+      T.nlds = std::max(0, std::min(64, want));
       G.nlds = std::min<uint32_t>(static_cast<uint32_t>(T.nlds), g->SL / G.H);
     }
     g->nlds = G.nlds;
@@ -2147,6 +2274,10 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     G.QL = T.qh;
     const uint64_t ql = static_cast<uint64_t>(G.nlds) * G.H;
     const uint64_t rest = qtot > ql + G.QL ? qtot - ql - G.QL : 0;
+    if (!getenv("PR_SEG"))  // (an explicit PR_SEG is taken as given and checked below)
+      while (NSLICE * (G.nlds + 1u + (rest + G.S - 1) / G.S) > static_cast<uint64_t>(MAX_NS) && G.S < (1u << 30))
+        G.S *= 2;
+    T.seg = G.S;
     g->nseg = G.nlds + 1u + static_cast<uint32_t>((rest + G.S - 1) / G.S);
     G.qb = bits_for(std::max({G.H, G.QL, G.S}));
     G.rb = bits_for(std::max<uint64_t>(lrows, 2));
@@ -2166,7 +2297,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&d_cnt, 2 + NG, err));
   HIPTRY(hipMemsetAsync(d_cnt, 0, 16, s));
   HIPTRY(hipMemsetAsync(d_cnt + 2, 0xFF, 8ull * NG, s));
-  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, lk_in, g->indeg, T.dropdeg);
+  if (nnz) hipLaunchKernelGGL(k_stream_keys, dim3(grid_loop(nnz)), dim3(BLOCK), 0, s, uniq, nnz, nb, inv, L, G, lk_in, g->indeg, T.dropdeg, T.keepdeg);
   if (T.dpull && p == 1 && nnz && lrows) {
     // direct-pull experiment: the column-major row groups of the rows below T.dpull
     span.next("prmi:build:direct-pull rows");
@@ -2254,7 +2385,7 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   }
   uint64_t lnnz = nnz;
   uint64_t* lk_alt = uniq;  // the unique keys are dead from here: sort scratch
-  if ((p > 1 || T.dropdeg) && nnz) {  // keep this rank's rows' edges (order-preserving select)
+  if ((p > 1 || T.dropdeg || T.keepdeg) && nnz) {  // keep this rank's rows' edges (order-preserving select)
     size_t tb = 0;
     HIPTRY(rocprim::select(nullptr, tb, lk_in, uniq, d_cnt, nnz, NotDropped(), s));
     TRY(tmp.ensure(tb, err));
@@ -2292,6 +2423,24 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   }
   g->gtask[NG] = static_cast<uint32_t>(tasks);
   g->ntask = static_cast<uint32_t>(tasks);
+  {
+    // Split point of each slice's L2 group for the two-part stream launch (p > 1): tasks
+    // before l2split[j] hold only L2-hot-range edges (x positions inside the hot prefix); the
+    // task that holds the first cold-segment edge and everything behind it need the whole x.
+    uint64_t* d_idx = nullptr;
+    TRY(dmalloc(&d_idx, NSLICE, err));
+    uint64_t hidx[NSLICE];
+    hipLaunchKernelGGL(k_cold_start, dim3(1), dim3(64), 0, s, lk, lnnz, G, d_idx);
+    HIPTRY(hipMemcpyAsync(hidx, d_idx, 8ull * NSLICE, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    (void)hipFree(d_idx);
+    for (uint32_t j = 0; j < NSLICE; ++j) {
+      const uint32_t l2g = j * (G.nlds + 1) + G.nlds;
+      const uint64_t a = g->gstart[l2g], b = g->gstart[l2g + 1];
+      const uint64_t i = std::min(std::max(hidx[j], a), b);
+      g->l2split[j] = i >= b ? g->gtask[l2g + 1] : g->gtask[l2g] + static_cast<uint32_t>((i - a) / TASK);
+    }
+  }
   g->stream_len = tasks * TASK;
   TRY(dmalloc(&g->d_gtask, NG + 1ull, err));
   TRY(dmalloc(&g->d_gstart, NG + 1ull, err));
@@ -2674,7 +2823,9 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   // persistent grid: 32 CUs per XCD, one 1024-thread block per CU (the LDS holds one x
   // block + the staging windows); PR_STREAM_WG blocks per CU without LDS blocks
   const int per_cu = A.nlds ? 1 : std::max(1, g->tune.stream_wg);
-  const dim3 gr(NSLICE * 32 * per_cu), bl(STREAM_BLOCK);
+  // (PR_STREAM_CUS < 32 leaves compute units of every XCD to other kernels, e.g. RCCL's)
+  const int cus = A.nlds ? std::max(1, std::min(32, g->tune.stream_cus)) : 32;
+  const dim3 gr(NSLICE * cus * per_cu), bl(STREAM_BLOCK);
   static bool attr_set = false;  // allow the >64 KB dynamic LDS request
   if (!attr_set) {
     for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<0, false, false>),
@@ -2723,7 +2874,7 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
 
 }  // namespace
 
-int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
+int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0, int part) {
   std::string* err = nullptr;
   const double* x_in = t == 1 ? (g->seeded ? g->x_seed : g->x_init) : g->xbuf[t & 1];
   StreamArgs S{};
@@ -2741,7 +2892,7 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   S.H = g->hot_h;
   S.colmask = g->tune.colmask;
   S.l2mode = static_cast<uint32_t>(g->tune.l2mode);
-  const bool stamps = t == 1 && !g->no_alloc && getenv("PR_STAMPS") && g->nlds && g->ntask;
+  const bool stamps = t == 1 && part == 0 && !g->no_alloc && getenv("PR_STAMPS") && g->nlds && g->ntask;
   const uint32_t nph = g->nlds + ((g->tune.l2mode == 1 || g->tune.l2w) ? 1u : 0u);
   std::vector<uint64_t> hst;
   uint64_t* dst = nullptr;
@@ -2754,10 +2905,29 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0) {
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
   S.wgdyn = static_cast<uint32_t>(env_int("PR_WGDYN", 1) != 0);
   S.l2late = static_cast<uint32_t>(g->tune.l2late);
+  S.part = static_cast<uint32_t>(part);
+  // A cut launch: part 1 = the first LDS phases + the L2-hot-range tasks, part 2 = the other
+  // phases + the cold-segment tasks, so both parts keep LDS-bound and L2-bound work side by
+  // side.  The L2 waves' work splits about 10 : 7 between the hot range and the cold segments
+  // (R-MAT scale 26), so part 1 takes 60 % of the phases (PR_XCUT percent).
+  uint32_t cut = g->nlds;
+  if (part != 0 && g->tune.l2w > 0) {
+    const int pct = std::max(1, std::min(100, env_int("PR_XCUT", 60)));
+    cut = std::min<uint32_t>(g->nlds, (g->nlds * static_cast<uint32_t>(pct) + 99u) / 100u);
+  }
+  S.ph_lo = part == 2 ? cut : 0u;
+  S.ph_hi = part == 1 ? cut : g->nlds;
+  uint64_t l2tasks = 0;
+  for (uint32_t j = 0; j < NSLICE; ++j) {
+    const uint32_t l2g = j * (g->nlds + 1) + g->nlds;
+    S.l2lo[j] = part == 2 ? g->l2split[j] : g->gtask[l2g];
+    S.l2hi[j] = part == 1 ? g->l2split[j] : g->gtask[l2g + 1];
+    l2tasks += S.l2hi[j] - S.l2lo[j];
+  }
   S.dbg = static_cast<uint32_t>(g->tune.dbg);
   S.x_bytes = static_cast<uint32_t>(std::min<uint64_t>(8ull * g->X, 0x7FFFFFFFull));
   if (ev0) HIPTRY(hipEventRecord(ev0, s));
-  if (g->ntask) launch_stream(g, S, s);
+  if (part == 2 ? (l2tasks != 0 || S.ph_lo < S.ph_hi) : g->ntask != 0) launch_stream(g, S, s);
   if (stamps) {  // PR_STAMPS: per-phase time of the stream launch (diagnostics only)
     HIPTRY(hipMemcpyAsync(hst.data(), dst, 8 * hst.size(), hipMemcpyDeviceToHost, s));
     HIPTRY(hipStreamSynchronize(s));
@@ -2880,7 +3050,7 @@ int dev_round_reduce(DevGraph* g, hipStream_t s, hipEvent_t ev1) {
 
 int dev_round_compute(DevGraph* g, int t, int mode, hipStream_t s, hipEvent_t ev0,
                       hipEvent_t ev1) {
-  int rc = dev_round_stream(g, t, s, ev0);
+  int rc = dev_round_stream(g, t, s, ev0, 0);
   if (!rc) rc = dev_round_rows(g, t, mode, 0, g->nb_rows, s);
   if (!rc) rc = dev_round_reduce(g, s, ev1);
   return rc;
@@ -2890,7 +3060,7 @@ int dev_round_single(DevGraph* g, int t, int mode, bool tracked, hipStream_t s, 
                      hipEvent_t ev1) {
   std::string* err = nullptr;
   if (g->p != 1) return PR_E_ARG;
-  int rc = dev_round_stream(g, t, s, ev0);
+  int rc = dev_round_stream(g, t, s, ev0, 0);
   if (!rc) rc = dev_round_rows(g, t, mode, 0, g->nb_rows, s);
   if (rc) return rc;
   if (g->dp_groups) {  // direct-pull experiment (timing only): inside the SpMV event bracket
@@ -2933,13 +3103,28 @@ int dev_round_single(DevGraph* g, int t, int mode, bool tracked, hipStream_t s, 
 // Exchange plan of the chunked x' exchange (p > 1): chunk k covers the slot positions
 // [P_{k-1}, P_k) of every slice sub-region of a rank's slot (the same on every rank), and the
 // class-A row blocks [b0, b1) that write them on this rank.
-std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K) {
+bool dev_can_split_stream(const DevGraph* g) {
+  // the hot prefix of a slice's q-space is a prefix of every slot sub-region only in the
+  // slice-major x layout, and a split needs LDS blocks (the two-role stream kernel)
+  return g->p > 1 && g->sm && g->nlds > 0;
+}
+
+std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K, bool hot_first) {
   std::vector<XChunk> out;
   const uint32_t p = static_cast<uint32_t>(g->p);
   const uint32_t nsub = g->sm ? NSLICE / p : 1u;          // sub-regions of a slot
   const uint64_t SLr = g->sm ? g->SL : g->maxA;            // entries per sub-region
   const uint32_t rows_per_pos = g->sm ? nsub : 1u;         // local rows per sub-region position
   K = std::max(1, std::min<int>(K, static_cast<int>(std::max<uint64_t>(SLr / CHUNK, 1))));
+  // hot_first: chunk 0 is exactly the hot prefix of every sub-region -- the positions the LDS
+  // blocks and the L2-hot range cover, all that the first part of the next round's stream
+  // launch reads -- and the other K - 1 chunks share the rest
+  uint64_t hot = 0;
+  if (hot_first && dev_can_split_stream(g)) {
+    hot = static_cast<uint64_t>(g->nlds) * g->hot_h + g->tune.qh;
+    hot = std::min<uint64_t>((hot + CHUNK - 1) / CHUNK * CHUNK, SLr);
+    if (K < 2 && hot < SLr) K = 2;
+  }
   auto block_row0 = [&](uint32_t b) -> uint64_t {
     if (b < g->row_nbH) return static_cast<uint64_t>(b) * g->row_rbH;
     return g->row_lH + static_cast<uint64_t>(b - g->row_nbH) * g->row_rb;
@@ -2948,6 +3133,7 @@ std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K) {
   uint32_t bprev = 0;
   for (int k = 0; k < K; ++k) {
     uint64_t P = (k == K - 1) ? SLr : ((SLr * (k + 1)) / K) / CHUNK * CHUNK;
+    if (hot) P = k == 0 ? hot : (k == K - 1 ? SLr : hot + ((SLr - hot) * k / (K - 1)) / CHUNK * CHUNK);
     if (P < prev) P = prev;
     // local rows below P map below P in every sub-region: l < P * rows_per_pos
     const uint64_t Lrow = P * rows_per_pos;
@@ -2969,7 +3155,11 @@ std::vector<XChunk> dev_exchange_plan(const DevGraph* g, int K) {
 int dev_sx_prepare(DevGraph* g, const std::vector<XChunk>& plan, std::string* err) {
   const uint32_t p = static_cast<uint32_t>(g->p), me = static_cast<uint32_t>(g->rank);
   const int K = static_cast<int>(plan.size());
-  if (g->sx_chunks == K) return PR_OK;
+  uint64_t sig = 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(K);
+  for (const XChunk& c : plan)
+    for (const XPiece& pc : c.pieces) sig = mix64(sig ^ (pc.off * 0x100000001B3ull + pc.cnt));
+  if (g->sx_chunks == K && g->sx_plan_sig == sig) return PR_OK;
+  g->sx_chunks = 0;
   if (p < 2 || g->sx_send.empty()) {
     if (err) *err = "sparse exchange: no cross-rank bitmaps (single rank?)";
     return PR_E_ARG;
@@ -3013,6 +3203,7 @@ int dev_sx_prepare(DevGraph* g, const std::vector<XChunk>& plan, std::string* er
     HIPTRY(hipMemcpy(g->sx_rpos, rp.data(), 4 * rp.size(), hipMemcpyHostToDevice));
   }
   g->sx_chunks = K;
+  g->sx_plan_sig = sig;
   return PR_OK;
 }
 
@@ -3062,6 +3253,32 @@ int dev_scatter_ranks(DevGraph* g, int iterations, hipStream_t s) {
     hipLaunchKernelGGL(k_scatter_ranks, dim3(grid_for(g->lrows)), dim3(BLOCK), 0, s, g->perm, g->r_loc[iterations & 1], g->lrows, layout_of(g), g->r_full);
   }
   HIPTRY(hipGetLastError());
+  return PR_OK;
+}
+
+// Host evaluation of the layout functions the kernels use (the same inline code, compiled for
+// the host): owner rank, local row and x position of internal vertices.
+int host_layout_map(int p, int rank, uint32_t nA, uint32_t nB, uint32_t nC, uint64_t cnt,
+                    const uint32_t* k, uint32_t* owner, uint32_t* local, uint64_t* xp,
+                    uint64_t dims[4]) {
+  if (p < 1 || rank < 0 || rank >= p) return PR_E_ARG;
+  if (static_cast<uint64_t>(nA) + nB + nC > 0xFFFFFFFFull) return PR_E_ARG;
+  const LayoutDims d = make_layout(p, rank, nA, nB, nC);
+  const uint32_t R = nA + nB;
+  for (uint64_t i = 0; i < cnt; ++i) {
+    const uint32_t v = k[i];
+    const bool row = v < R, col = v < nA || (v >= R && v - R < nC);
+    if (!row && !col) return PR_E_ARG;  // class-D vertices have neither a row nor an x entry
+    if (owner) owner[i] = row ? owner_of(d.L, v) : 0xFFFFFFFFu;
+    if (local) local[i] = row ? local_of(d.L, v) : 0xFFFFFFFFu;
+    if (xp) xp[i] = col ? xpos(d.L, v) : ~0ull;
+  }
+  if (dims) {
+    dims[0] = d.L.maxA;
+    dims[1] = d.X;
+    dims[2] = d.lrows;
+    dims[3] = d.lA;
+  }
   return PR_OK;
 }
 
@@ -3177,6 +3394,70 @@ int dev_topk_candidates(DevGraph* g, uint64_t k, std::vector<uint32_t>* ids,
   return PR_OK;
 }
 
+
+// One wave that sleeps for about `us` microseconds (s_memrealtime ticks at 100 MHz); bounded by
+// an iteration cap, so it ends whatever the clock does.  Measurements only.
+__global__ void k_delay(uint32_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t i = 0; i < (1u << 22); ++i) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
+    __builtin_amdgcn_s_sleep(64);
+  }
+}
+int dev_delay_us(int us, hipStream_t s) {
+  std::string* err = nullptr;
+  if (us > 0) hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, static_cast<uint32_t>(std::min(us, 1000000)) * 100u);
+  HIPTRY(hipGetLastError());
+  return PR_OK;
+}
+
+int dev_selftest_lds_order(uint32_t cases, uint32_t launches, hipStream_t s, uint64_t* copies,
+                           uint64_t* differing, uint64_t* lane_order_cases, std::string* err) {
+  constexpr uint32_t GRID = 2048;  // 8 workgroups per CU: every CU and XCD takes part
+  const uint64_t nw = static_cast<uint64_t>(GRID) * (BLOCK / 64);
+  uint64_t* d = nullptr;
+  TRY(dmalloc(&d, nw * ST_ROWS, err));
+  struct Free {
+    void* p;
+    ~Free() { (void)hipFree(p); }
+  } fr{d};
+  std::vector<uint64_t> h(nw * ST_ROWS);
+  *copies = *differing = *lane_order_cases = 0;
+  for (uint32_t c = 0; c < cases; ++c) {
+    // the sum in ascending lane order, one rounding per add (what a serial loop gives)
+    double seq[ST_ROWS] = {0};
+    for (uint32_t l = 0; l < 64; ++l) {
+      uint32_t row;
+      double v;
+      st_case(c, l, &row, &v);
+      seq[row] += v;
+    }
+    uint64_t first[ST_ROWS];
+    bool have = false;
+    for (uint32_t it = 0; it < launches; ++it) {
+      hipLaunchKernelGGL(k_lds_order, dim3(GRID), dim3(BLOCK), 0, s, c, d);
+      HIPTRY(hipGetLastError());
+      HIPTRY(hipMemcpyAsync(h.data(), d, 8 * h.size(), hipMemcpyDeviceToHost, s));
+      HIPTRY(hipStreamSynchronize(s));
+      if (!have) {
+        memcpy(first, h.data(), sizeof(first));
+        have = true;
+      }
+      for (uint64_t w = 0; w < nw; ++w) {
+        ++*copies;
+        if (memcmp(&h[w * ST_ROWS], first, sizeof(first)) != 0) ++*differing;
+      }
+    }
+    bool same = true;
+    for (int r = 0; r < ST_ROWS; ++r) {
+      uint64_t b;
+      memcpy(&b, &seq[r], 8);
+      same = same && b == first[r];
+    }
+    if (same) ++*lane_order_cases;
+  }
+  return PR_OK;
+}
 
 int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s, std::string* err) {
   const Layout L = layout_of(g);

@@ -137,6 +137,10 @@ def lib():
         "pr_ext_round": (I32, [P, I32, P]),
         "pr_ext_complete": (I32, [P, I32, P, C.POINTER(I32)]),
         "pr_ext_end": (I32, [P, C.POINTER(Stats)]),
+        "pr_progress": (I32, [P, C.POINTER(I32), C.POINTER(I32)]),
+        "pr_comm_query": (I32, [P, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32)]),
+        "pr_layout_map": (I32, [I32, I32, U32, U32, U32, U64, P, P, P, P, P]),
+        "pr_selftest_sum_order": (I32, [P, U32, U32, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
         "pr_ingest_files": (I32, [P, C.c_char_p, C.c_char_p]),
         "pr_ingest_buffers": (I32, [P, C.c_char_p, SZ, C.c_char_p, SZ]),
         "pr_load_edges": (I32, [P, P, P, U64, U32, P, U64]),
@@ -194,6 +198,22 @@ def format_double(v: float) -> str:
     return buf.raw[:n].decode()
 
 
+def layout_map(n_ranks: int, rank: int, n_a: int, n_b: int, n_c: int, ids):
+    """The engine's row deal and x layout on the host (``pr_layout_map``): for internal vertex
+    ids returns (owner rank, local row, x position) arrays and the dims dict."""
+    k = np.ascontiguousarray(ids, np.uint32)
+    owner = np.zeros(len(k), np.uint32)
+    local = np.zeros(len(k), np.uint32)
+    xp = np.zeros(len(k), np.uint64)
+    dims = np.zeros(4, np.uint64)
+    rc = lib().pr_layout_map(n_ranks, rank, n_a, n_b, n_c, len(k), _ptr(k), _ptr(owner),
+                             _ptr(local), _ptr(xp), _ptr(dims))
+    if rc:
+        raise PageRankError(rc, f"pr_layout_map failed ({rc})")
+    return owner, local, xp, {"max_a": int(dims[0]), "x_len": int(dims[1]),
+                              "local_rows": int(dims[2]), "local_a": int(dims[3])}
+
+
 def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     rc = lib().pr_comm_unique_id(buf)
@@ -243,6 +263,31 @@ class Engine:
     def comm_init_external(self):
         """Exchange rounds through the caller (pr_ext_*), e.g. a torch.distributed group."""
         self._check(lib().pr_comm_init_external(self._h))
+
+    def progress(self) -> Tuple[int, int]:
+        """(rounds enqueued, rounds finished) of the running or last round loop; safe to call
+        from another thread while ``run`` blocks."""
+        enq, done = C.c_int32(0), C.c_int32(0)
+        h = self._h
+        if not h:
+            return 0, 0
+        lib().pr_progress(h, C.byref(enq), C.byref(done))
+        return enq.value, done.value
+
+    def selftest_sum_order(self, cases: int = 64, launches: int = 20) -> Dict[str, int]:
+        """Bit-compare the LDS double-add order of the row launch over many waves and launches
+        (pr_selftest_sum_order)."""
+        a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        self._check(lib().pr_selftest_sum_order(self._h, cases, launches, C.byref(a), C.byref(b),
+                                                C.byref(c)))
+        return {"copies": a.value, "differing": b.value, "lane_order_cases": c.value, "cases": cases}
+
+    def comm_query(self) -> Dict[str, object]:
+        """Transport of this context and, for RCCL, the communicator's own rank count."""
+        tr, n, r = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        self._check(lib().pr_comm_query(self._h, C.byref(tr), C.byref(n), C.byref(r)))
+        return {"transport": ("none", "rccl", "local-group", "external")[tr.value],
+                "comm_ranks": n.value, "comm_rank": r.value}
 
     def run_external(self, iterations: int, allgather, tol: float = 0.0) -> Dict[str, float]:
         """The round loop with a caller-supplied all-gather: ``allgather(send) -> recv`` takes

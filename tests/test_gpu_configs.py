@@ -4,7 +4,8 @@ These are the benchmark graphs themselves (R-MAT, Graph500 a/b/c/d, edge factor 
 by the device generator and by the oracle's own Philox stream from the same seed:
 
   cfg3  scale 24, seed 3, run to relative L1 residual <= 1e-8 (BASELINE.json configs[2])
-  cfg4  scale 26, seed 4, T = 10 (configs[3]; the graph bench.py measures, seed 4)
+  cfg4  scale 26, seed 4, T = 10 (configs[3]; the graph bench.py measures, seed 4), on one
+        rank against the oracle and as 2 / 4 / 8-rank groups (sparse exchange) against one rank
   cfg5  scale 28, seed 5, T = 10, the 8-rank row partition (configs[4])
 
 Bars (north_star): bit-exact edge set and degrees (PageRank.java:42, :103-108); identical
@@ -95,6 +96,42 @@ def test_cfg4_scale26_ten_rounds(P, O):
     parity.assert_same_order_mod_ties(top, rmat_top_rows(exp, TOPK))
     print(f"cfg4: nnz {st['nnz']}, worst rel {worst:.2e}, {st['gteps']:.1f} GTEPS, "
           f"{time.time() - t0:.0f} s")
+
+
+@pytest.fixture(scope="module")
+def cfg4_single(P):
+    """cfg4 on one rank: ranks after 10 rounds and the top-1000 rows (checked against the
+    oracle by test_cfg4_scale26_ten_rounds)."""
+    eng = P.Engine()
+    eng.generate_rmat(26, 16, 4)
+    info = eng.info()
+    eng.run(10)
+    r1, top1 = eng.ranks(), engine_top_rows(eng, TOPK)
+    eng.close()
+    return info, r1, top1
+
+
+@pytest.mark.parametrize("p", [2, 4, 8])
+def test_cfg4_scale26_rank_groups(P, cfg4_single, p):
+    """The row partition, x layout and sparse exchange lists the 2/4/8-GPU benchmark uses, at
+    the benchmark's own size (PageRank.java:139 reduceByKey across executors, :187-189): p ranks
+    on this GPU against one rank."""
+    t0 = time.time()
+    info, r1, top1 = cfg4_single
+    assert os.environ.get("PR_SPARSE_X", "1") != "0"            # the sparse exchange is on
+    grp = P.LocalGroup(p)
+    grp.each("generate_rmat", 26, 16, 4)
+    infos = [m.info() for m in grp.members]
+    assert sum(x["local_nnz"] for x in infos) == info["nnz"]     # every edge on one rank
+    assert sum(x["local_rows"] for x in infos) == info["n_rows"]
+    assert max(x["local_nnz"] for x in infos) <= 1.02 * info["nnz"] / p   # balanced deal
+    st = grp.run(10)
+    assert st["iterations"] == 10
+    rp = grp.members[p - 1].ranks()
+    worst = parity.assert_ranks_close(rp, r1, rtol=1e-12)
+    parity.assert_same_order_mod_ties(engine_top_rows(grp.members[0], TOPK), top1, rtol=1e-12)
+    grp.close()
+    print(f"cfg4 at {p} ranks: worst rel vs 1 rank {worst:.2e}, {time.time() - t0:.0f} s")
 
 
 def test_cfg5_scale28_eight_rank_layout(P, O):

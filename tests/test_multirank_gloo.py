@@ -1,14 +1,17 @@
-"""World-size-2 CPU rehearsal (gloo) of the engine's multi-GPU protocol (DESIGN.md §5).
+"""World-size-2 CPU rehearsal (gloo) of the engine's multi-GPU protocol.
 
-The engine deals internal rows to ranks in chunks of 16 (chunk c = k // 16 goes to rank
-c % p), writes each rank's new contribution values into its own contiguous slot of x
-(A-row k at owner(k)*maxA + local(k), C-vertex k at p*maxA + (k - R), maxA a multiple of
-16), all-gathers the slots in place, and
-sums the per-rank exact dangling records in any order.  This test replays that protocol
-with numpy on two gloo ranks and checks: (1) the assembled ranks are bit-identical to the
-same protocol at p = 1, (2) they match the oracle within 1e-9, (3) every edge and row is
-owned by exactly one rank.  The real RCCL path runs on the driver's 8-GPU node; the same
-layout is exercised on one GPU by tests/test_gpu_parity.py::test_rank_group_*.
+Two gloo ranks on the CPU run the round protocol of a 2-GPU job -- rows dealt to ranks, every
+rank's new contribution values written into its own slot of x, the slots all-gathered in place,
+the exact dangling records combined in any order -- with the layout taken from the engine
+itself: owner rank, local row and x position of every vertex come from ``pr_layout_map``, the
+host build of the very functions the kernels use (engine.hip owner_of / local_of / xpos), not
+from a model of them.  The arithmetic of a round is numpy (there is no GPU here).  Checks:
+(1) both ranks derive the same x layout and it is collision-free, (2) local rows are dense and
+a rank's class-A rows land exactly in its own slot, (3) every edge and row is owned by exactly
+one rank, (4) the assembled ranks are bit-identical to the same protocol at p = 1 and match
+the oracle within 1e-9.  The device side of the same protocol runs in tests/test_gpu_multiproc.py
+(gloo worlds of 2 and 4 processes on one GPU) and tests/test_gpu_parity.py (rank groups); the
+RCCL transport needs one GPU per rank (tests/test_gpu_rccl.py).
 """
 import math
 import os
@@ -36,60 +39,45 @@ def internal_order(src, dst, n, mapw):
 
 
 def protocol(rank, p, src, dst, n, mapw, n_tot, allgather, gather_records):
+    import prmi355x as P
     perm, inv, (nA, nB, nC, _nD), outd, ind, dang_w = internal_order(src, dst, n, mapw)
     R = nA + nB
-    CH = 16
-
-    def owner(k):
-        return (k // CH) % p
-
-    def local(k):
-        return ((k // CH) // p) * CH + k % CH
-
-    # slice-major x (p divides 8): rank slot -> slice region (chunk % 8) -> chunk order
-    NS = 8
-    SL = CH * -(-(-(-nA // CH)) // NS)
-    SLC = CH * -(-(-(-nC // CH)) // NS)
-    maxA = (NS // p) * SL
-    X = p * maxA + NS * SLC
-
-    def xpos(k):
-        c = k // CH
-        kc = k - R
-        cc = kc // CH
-        a = ((c % NS) % p) * maxA + ((c % NS) // p) * SL + (c // NS) * CH + k % CH
-        b = p * maxA + (cc % NS) * SLC + (cc // NS) * CH + kc % CH
-        return np.where(k < nA, a, b)
-
-    def xslot(l):                                           # local row -> offset in own slot
-        c = (l // CH) * p + rank
-        return ((c % NS) // p) * SL + (c // NS) * CH + l % CH
-
+    # the engine's own deal and x layout (host build of the kernels' layout functions)
     allrows = np.arange(R)
-    own = allrows[owner(allrows) == rank]                   # internal rows of this rank
-    assert np.array_equal(local(own), np.arange(len(own)))  # local rows are dense
+    owner, local, _xp, dims = P.layout_map(p, rank, nA, nB, nC, allrows)
+    maxA, X = dims["max_a"], dims["x_len"]
+    cols_all = np.concatenate([np.arange(nA), np.arange(R, R + nC)])
+    _o, _l, xp_cols, _d = P.layout_map(p, rank, nA, nB, nC, cols_all)
+    xpos = np.full(n, -1, np.int64)
+    xpos[cols_all] = xp_cols.astype(np.int64)
+    assert len(np.unique(xp_cols)) == len(cols_all) and xp_cols.max() < X     # collision-free
+    assert np.all(xpos[:nA] < p * maxA) and np.all(xpos[R:R + nC] >= p * maxA)  # slots, then C
+
+    own = allrows[owner == rank]                            # internal rows of this rank
+    assert len(own) == dims["local_rows"] and int((own < nA).sum()) == dims["local_a"]
+    assert np.array_equal(local[owner == rank], np.arange(len(own)))   # local rows are dense
     kd, ks = inv[dst], inv[src]
-    mine = owner(kd) == rank
-    order = np.lexsort((ks[mine], local(kd[mine])))        # (local row, internal source)
-    lrow = local(kd[mine])[order]
+    mine = owner[kd] == rank
+    order = np.lexsort((ks[mine], local[kd[mine]]))        # (local row, internal source)
+    lrow = local[kd[mine]][order].astype(np.int64)
     lsrc = ks[mine][order]
-    col = xpos(lsrc)
+    col = xpos[lsrc]
     rp = np.zeros(len(own) + 1, np.int64)
     np.add.at(rp, lrow + 1, 1)
     rp = np.cumsum(rp)
     x = np.zeros(X)
-    cols_all = np.concatenate([np.arange(nA), np.arange(R, R + nC)])
-    x[xpos(cols_all)] = 1.0 / outd[perm[cols_all]]
+    x[xpos[cols_all]] = 1.0 / outd[perm[cols_all]]
     r_loc = np.zeros(len(own))
     w_own = dang_w[perm[own]]
     a = float(dang_w.sum()) / n_tot
+    isA = own < nA
+    slot_of = xpos[own[isA]] - rank * maxA                   # own class-A rows: inside own slot
+    assert slot_of.min(initial=0) >= 0 and slot_of.max(initial=0) < maxA
     for _t in range(ROUNDS):
         c = np.array([math.fsum(x[col[rp[l]:rp[l + 1]]]) for l in range(len(own))])
         r_loc = np.where(c > 0, 0.15 + (c + a) * 0.85, 0.0)
         slot = np.zeros(maxA)
-        isA = own < nA
-        slot[xslot(np.nonzero(isA)[0])] = r_loc[isA] / outd[perm[own[isA]]]
-        assert np.array_equal(rank * maxA + xslot(np.nonzero(isA)[0]), xpos(own[isA]))
+        slot[slot_of] = r_loc[isA] / outd[perm[own[isA]]]
         xn = np.zeros(X)
         xn[:p * maxA] = allgather(slot)                   # in-place all-gather of slots
         x = xn
@@ -98,10 +86,15 @@ def protocol(rank, p, src, dst, n, mapw, n_tot, allgather, gather_records):
         a = math.fsum(r * w for r, w in recs) / n_tot      # exact, order-free combine
     full = np.zeros(n)
     full[perm[own]] = r_loc
-    return full, (len(own), len(lsrc))
+    return full, (len(own), len(lsrc)), xp_cols
 
 
 def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for d in ("page-rank-and-tfidf-using-apache-spark_amd", "oracle"):
+        if os.path.join(root, d) not in sys.path:
+            sys.path.insert(0, os.path.join(root, d))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -123,7 +116,11 @@ def _worker(rank, world, port, q):
         dist.all_gather_object(out, recs)
         return [r for part in out for r in part]
 
-    full, owned = protocol(rank, world, src, dst, n, mapw, n, allgather, gather_records)
+    full, owned, xp_cols = protocol(rank, world, src, dst, n, mapw, n, allgather, gather_records)
+    # every rank derives the same x layout
+    lay = [None] * world
+    dist.all_gather_object(lay, xp_cols.tobytes())
+    assert all(b == lay[0] for b in lay)
     t = torch.from_numpy(full)
     dist.all_reduce(t)                                    # one nonzero per page: exact
     if rank == 0:
@@ -141,7 +138,7 @@ def _free_port():
         return sk.getsockname()[1]
 
 
-def test_two_rank_protocol_matches_single_rank_and_oracle(oracle_mod):
+def test_two_rank_protocol_matches_single_rank_and_oracle(oracle_mod, engine_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -160,8 +157,8 @@ def test_two_rank_protocol_matches_single_rank_and_oracle(oracle_mod):
     dst = (k >> np.uint64(32)).astype(np.int64)
     src = (k & np.uint64(0xFFFFFFFF)).astype(np.int64)
     n = 1 << SCALE
-    full1, own1 = protocol(0, 1, src, dst, n, np.ones(n, np.int64), n,
-                           lambda sl: sl, lambda recs: recs)
+    full1, own1, _xp = protocol(0, 1, src, dst, n, np.ones(n, np.int64), n,
+                                lambda sl: sl, lambda recs: recs)
     assert np.array_equal(full1.view(np.uint64), full2.view(np.uint64))
     assert sum(o[0] for o in owned) == own1[0] and sum(o[1] for o in owned) == own1[1] == len(k)
     exp = O.Graph.from_rmat(SCALE, EF, SEED).run(ROUNDS)["ranks"]
