@@ -582,7 +582,10 @@ __device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[
 // NT: 2 = non-temporal piece stores.  SPLIT: dedicated L2 waves (A.l2w).  STAMPS: PR_STAMPS
 // diagnostics.  The variants are separate instantiations so that the default one carries no
 // register cost for the others.
-template <int NT, bool SPLIT, bool STAMPS, int NTC = 0, bool LEAN = false>
+// EXP: the A/B switches of round 3 each live in an instantiation of their own (1 = PR_L2LATE=1,
+// 2 = PR_L2LATE=2, 4 = PR_DBG=8192); together inside the default one they cost 12 VGPRs and
+// pushed its hot loop into scratch spills (1.65 -> 1.99 ms per launch).
+template <int NT, bool SPLIT, bool STAMPS, int NTC = 0, bool LEAN = false, int EXP = 0>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
   const uint32_t j = blockIdx.x % NSLICE;
@@ -748,7 +751,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       if (A.dbg & 4u) b = 0;
       if (lane == 0) b |= 1u;  // a task always starts a piece
       // next task's stream words first: they stay in flight while this task gathers
-      const bool late = l2role && A.l2late == 1u;
+      const bool late = (EXP & 1) != 0 && l2role && A.l2late == 1u;
       if (un < nu && !late) fetch_u(un);
       const uint32_t unn = dyn ? (un < nu ? claim() : nu) : un + nw;
       double v[EPL];
@@ -800,7 +803,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // PR_DBG=8192 (timing only, wrong sums): a task made almost only of single-edge pieces
     // stores its sixteen gathered values per lane as if lane l's edge k were piece 64 k + l --
     // the store pattern of a column-major all-singles task: no sums, no scan, no staging
-    const bool fastd = (A.dbg & 8192u) != 0u && total >= 768u;
+    const bool fastd = (EXP & 4) != 0 && (A.dbg & 8192u) != 0u && total >= 768u;
     if (fastd) {
 #pragma unroll
       for (int k = 0; k < EPL; ++k)
@@ -896,7 +899,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     }  // !fastd
       // PR_L2LATE=2 (A/B): the L2-role waves wait for their piece stores right here; the cost
       // bounds what the gathers' in-order wait can lose to stores still in flight
-      if (l2role && A.l2late == 2u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if ((EXP & 2) != 0 && l2role && A.l2late == 2u) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       u = un;
       un = unn;
     }
@@ -2861,6 +2864,23 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
                           reinterpret_cast<const void*>(&spmv_stream<0, true, false, 0, true>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     lattr = true;
+  }
+  const int exper = g->tune.l2late == 1 ? 1 : (g->tune.l2late == 2 ? 2 : ((g->tune.dbg & (8192 | 16384)) ? 4 : 0));
+  // (PR_DBG=16384 runs the PR_DBG=8192 instantiation with its fast path off: that variant
+  // carries 22 spilled registers, so its A/B partner must carry them too)
+  if (exper && g->tune.nt == 2 && split && lean && !st) {
+    static bool eattr = false;
+    if (!eattr) {
+      for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 1>),
+                            reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 2>),
+                            reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 4>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      eattr = true;
+    }
+    if (exper == 1) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, 1>), gr, bl, lds, s, A);
+    else if (exper == 2) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, 2>), gr, bl, lds, s, A);
+    else hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, 4>), gr, bl, lds, s, A);
+    return;
   }
   if (g->tune.nt == 0 && split && lean && !st) hipLaunchKernelGGL((spmv_stream<0, true, false, 0, true>), gr, bl, lds, s, A);
   else if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);

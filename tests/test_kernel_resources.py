@@ -1,0 +1,50 @@
+"""Register budget of the shipped SpMV kernels (CPU: reads the built engine object).
+
+The stream launch runs one 1024-thread workgroup per compute unit, so it has 128 VGPRs per
+lane and not one more: a change that pushes the default instantiation over that line spills its
+hot loop to scratch and costs 20 % of the launch without failing any parity test.  This test
+fails instead: the default stream kernel and the three row kernels must carry no spilled
+registers and no scratch.
+"""
+import os
+import re
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OBJ = os.path.join(ROOT, "page-rank-and-tfidf-using-apache-spark_amd", "_build", "engine.o")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def kernel_notes():
+    with tempfile.TemporaryDirectory() as tmp:
+        obj = os.path.join(tmp, "engine.o")
+        with open(OBJ, "rb") as f, open(obj, "wb") as g:
+            g.write(f.read())
+        subprocess.run([os.path.join(LLVM, "llvm-objdump"), "--offloading", obj], check=True,
+                       capture_output=True, cwd=tmp)
+        co = [n for n in os.listdir(tmp) if "amdgcn" in n]
+        assert len(co) == 1, os.listdir(tmp)
+        out = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", os.path.join(tmp, co[0])],
+                             check=True, capture_output=True, text=True).stdout
+    # one metadata block per kernel; a block's fields come in alphabetical order
+    blocks = re.split(r"\n\s+- \.", out)
+    kernels = {}
+    for b in blocks:
+        nm = re.search(r"\.name:\s+(\S+)", b)
+        if not nm or ".vgpr_count" not in b:
+            continue
+        kernels[nm.group(1)] = {k: int(v) for k, v in re.findall(
+            r"\.(vgpr_count|vgpr_spill_count|sgpr_spill_count|private_segment_fixed_size):\s+(\d+)", b)}
+    return kernels
+
+
+def test_default_spmv_kernels_do_not_spill(engine_mod):
+    ks = kernel_notes()
+    stream = [n for n in ks if "spmv_stream" in n and n.endswith("ILi2ELb1ELb0ELi0ELb1ELi0EEEvNS_10StreamArgsE")]
+    rows = [n for n in ks if "spmv_rows" in n]
+    assert len(stream) == 1 and len(rows) == 3, sorted(ks)
+    for n in stream + rows:
+        k = ks[n]
+        assert k["vgpr_spill_count"] == 0 and k["private_segment_fixed_size"] == 0, (n, k)
+        assert k["vgpr_count"] <= 128, (n, k)
