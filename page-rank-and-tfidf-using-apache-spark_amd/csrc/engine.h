@@ -81,8 +81,8 @@ struct Tuning {
   uint32_t rxg = 16;     // PR_RXG: consecutive row-launch blocks per XCD (1 = round-robin)
   uint32_t heavy_deg = 128; // PR_HDEG: rows with in-degree >= this get heavy blocks (0 = none)
   int nlds = 20;        // PR_NLDS: LDS blocks per slice (each swept with its own LDS fill).  Unset,
-                        // the build sizes it to the graph: the hottest ~11.5 % of a slice's
-                        // class-A columns (20 blocks at R-MAT scale 26 on one rank)
+                        // the build sizes it to the graph: 0.41 B^0.77 for a slice of B blocks'
+                        // worth of class-A columns (21 blocks at R-MAT scale 26 on one rank)
   uint32_t seg = 262144;  // PR_SEG: cold segment length per slice (x entries, 2 MiB)
   // PR_NT: 2 = non-temporal piece stores (they stop evicting x from the L2s: +3 %), 0 =
   // regular stores.  Non-temporal stream loads and LDS fills were measured slower.

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <string.h>
@@ -2255,17 +2256,19 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
     G.nlds = 0;
     if (g->sm && g->X < (1ull << 28) && T.hot_lds > 0) {
       G.H = std::min<uint32_t>(HOT_MAX, T.hot_lds) & ~1u;  // even: 16-byte LDS-DMA fills
-      // LDS blocks per slice: the measured optimum covers the hottest ~11.5 % of a slice's
-      // class-A columns whatever the size of the graph (R-MAT scale 22 / 24 / 26 / 28 on one
-      // rank: 2 / 6 / 20 / 64 blocks; a fixed 20 cost 33 % at scale 22 and 22 % at scale 28),
-      // and a rank of p >= 2 takes 0.75 x (p = 2) or 0.6 x (p >= 4) of that: its share of every
-      // phase shrinks with p while the per-phase cost stays (scale 26: 15 and 12; scale 28 at
-      // 8 ranks: 40 against 24 and 12).  Cold segments widen until the row launch's stream
-      // table holds every (slice, segment).
+      // LDS blocks per slice follow the graph: with B = (class-A columns of a slice) / H, the
+      // measured optimum on one rank is 1 / 3 / 8 / 20 / 52-64 blocks at R-MAT scale 20 / 22 /
+      // 24 / 26 / 28 (B = 3.5 / 13 / 46 / 168 / 610), i.e. 0.41 B^0.77: the hot share worth an
+      // LDS fill shrinks slowly as the graph grows (23 % of a slice's columns at scale 22, 9 %
+      // at scale 28).  A fixed 20 cost 25 % at scale 22 and 13 % at scale 28.  A rank of p >= 2
+      // takes 0.75 x (p = 2) or 0.6 x (p >= 4) of that: its share of every phase shrinks with
+      // p while the per-phase cost stays (scale 26: 15 and 12; scale 28 at 8 ranks: 40 against
+      // 24 and 12).  Cold segments widen until the row launch's stream table holds every
+      // (slice, segment).
       int want = nlds_env;
       if (want < 0) {
         const double f = p >= 4 ? 0.6 : (p >= 2 ? 0.75 : 1.0);
-        want = static_cast<int>(0.115 * f * static_cast<double>(g->SL) / G.H + 0.5);
+        want = static_cast<int>(0.41 * f * std::pow(static_cast<double>(g->SL) / G.H, 0.77) + 0.5);
         want = std::max(1, want);
       }
       T.nlds = std::max(0, std::min(64, want));
