@@ -37,11 +37,16 @@ def _port() -> int:
 
 
 @pytest.mark.skipif(_gpus() < 2, reason="needs 2 GPUs (RCCL rejects two ranks on one device)")
-@pytest.mark.parametrize("sparse", ["0", "1"])
-def test_rccl_two_ranks_match_one_rank(engine_mod, oracle_mod, tmp_path, monkeypatch, sparse):
-    """sparse = 1 forces the sparse x' exchange (its RCCL count check, packed send/recv)."""
+@pytest.mark.parametrize("sparse,tiny", [("0", False), ("1", False), ("1", True), ("0", True)])
+def test_rccl_two_ranks_match_one_rank(engine_mod, oracle_mod, tmp_path, monkeypatch, sparse, tiny):
+    """sparse = 1 forces the sparse x' exchange (its RCCL count check, packed send/recv); tiny
+    = a stream geometry with LDS blocks on this small graph, so the ranks run the overlapped
+    schedule (cut stream launch, hot-first exchange plan) over RCCL."""
     P, O = engine_mod, oracle_mod
     monkeypatch.setenv("PR_SPARSE_X", sparse)
+    if tiny:
+        for k, v in (("PR_HOTLDS", "256"), ("PR_NLDS", "6"), ("PR_QH", "1024"), ("PR_SEG", "512")):
+            monkeypatch.setenv(k, v)
     a, m = G.wiki_text(seed=3, pages=20_000, arcs_target=200_000)
     (tmp_path / "arcs").write_bytes(a)
     (tmp_path / "map").write_bytes(m)
