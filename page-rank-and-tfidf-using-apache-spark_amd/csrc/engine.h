@@ -99,6 +99,10 @@ struct Tuning {
                         // (timing only, single rank; engine.hip spmv_dpull)
   uint32_t dropdeg = 0; // PR_DROPDEG: rows below this in-degree leave the streams (timing only)
   uint32_t keepdeg = 0; // PR_KEEPDEG: rows at or above this in-degree leave the streams (timing only)
+  int dyntail = 100;    // PR_DYNTAIL: percent of the LDS phases whose tasks go to the slice's
+                        // workgroups in fixed shares; the later phases are claimed slice-wide
+  int dyng = 4;         // PR_DYNG: tasks per slice-wide claim
+  int dynl2 = 0;        // PR_DYNL2: the L2-role waves claim their tasks slice-wide too
   int stream_cus = 32;  // PR_STREAM_CUS: stream workgroups (= compute units) per XCD
   int l2late = 0;       // PR_L2LATE: L2-role waves prefetch the next task's columns after
                         // their gathers instead of before (see StreamArgs::l2late)
@@ -179,6 +183,8 @@ struct DevGraph {
   double* r_loc[2] = {nullptr, nullptr};
   double* r_full = nullptr;       // [n] by original id (output staging)
   uint64_t* shards = nullptr;     // [NSHARD][REC_WORDS]
+  uint32_t* stream_cnt = nullptr; // [NSLICE * 72] slice-wide task counters of the stream launch
+                                  // (zeroed by the round's record reduction)
   uint64_t* rec_local = nullptr;  // [REC_WORDS]
   uint64_t* rec_all = nullptr;    // [p][REC_WORDS]
   // sparse x' exchange (p > 1): which class-A x entries each rank's edges reference, computed

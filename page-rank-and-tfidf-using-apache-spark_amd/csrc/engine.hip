@@ -409,6 +409,11 @@ struct StreamArgs {
                              // L2 tasks are shared out over the LDS phases, see l2mode)
   uint32_t wgdyn;            // PR_WGDYN: LDS waves claim their workgroup's tasks from an LDS
                              // counter (1) or take them round-robin (0)
+  uint32_t* gcnt;            // [NSLICE * GCNT] task counters of the slice-wide claims (zero at launch)
+  uint32_t dyng;             // tasks per slice-wide claim (PR_DYNG)
+  uint32_t l2dyn;            // PR_DYNL2: the L2-role waves claim their tasks slice-wide as well
+  uint32_t dyn0;             // LDS phases >= dyn0 deal their tasks to the slice's workgroups from
+                             // gcnt instead of in fixed shares (PR_DYNTAIL)
   uint32_t l2lo[NSLICE];     // L2-group tasks [l2lo, l2hi) of each slice this launch sweeps
   uint32_t l2hi[NSLICE];
   uint32_t ph_lo, ph_hi;     // LDS phases [ph_lo, ph_hi) this launch runs (all of them unless
@@ -421,6 +426,8 @@ struct StreamArgs {
                              // for it), A/B switch
 };
 constexpr int STREAM_BLOCK = 1024;
+constexpr uint32_t GCNT = 72;      // slice-wide task counters per slice: one per LDS phase (<= 64),
+                                   // slots 64 / 65 for the L2 role (whole or first part / second part)
 constexpr int STG = 256;           // per-wave LDS staging window for piece stores (doubles)
 // LDS left for the x block: H entries + a zero slot (index H, the 16-bit padding column)
 constexpr uint32_t HOT_MAX = 20480 - (STREAM_BLOCK / 64) * STG - 8;
@@ -611,6 +618,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // (task u to workgroup u mod 32) and the workgroup's LDS waves claim its tasks from this
   // counter, so no wave idles at the phase barrier while a sibling still has a backlog
   uint32_t& task_cnt = *reinterpret_cast<uint32_t*>(hot + A.H + 2);
+  // slice-wide claims: "this phase has no task left" flags, one per phase parity
+  uint32_t* skipf = reinterpret_cast<uint32_t*>(hot + A.H + 3);
   const bool wgdyn = split && !l2role && A.wgdyn != 0u;
   const uint32_t qwg = blockIdx.x / NSLICE, nqwg = gridDim.x / NSLICE;
   uint32_t bar_gen = 0;
@@ -691,8 +700,13 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   for (uint32_t gi = g0; gi < g1; ++gi) {
     uint32_t tb = l2b, te = l2b, rb = l2b, re = l2e;  // LDS-block tasks, L2 share
     uint64_t lbase = 0;
+    bool gdyn = false;
+    uint32_t gslot = gi;  // counter of this phase's slice-wide claims
     if (onlyl2 || (gi == A.nlds && (l2last || l2role))) {
-      // the L2 phase / role: no LDS block, the whole L2 group (segments swept in order)
+      // the L2 phase / role: no LDS block, the whole L2 group (segments swept in order); with
+      // l2dyn its tasks go to the slice's L2 waves in claim order, front to back
+      gdyn = l2role && A.l2dyn != 0u && A.gcnt != nullptr;
+      gslot = A.part == 2u ? 65u : 64u;
     } else if (A.nlds) {
       tb = A.gtask[j * ngs + gi];
       te = A.gtask[j * ngs + gi + 1];
@@ -701,7 +715,16 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       re = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * (gi + 1)) / A.nlds);
       if (l2last || split) rb = re = l2b;
       const uint32_t hb = A.hot_base[j] + gi * A.H;
-      block_barrier();  // every wave is done with the previous block
+      // Late phases deal their tasks slice-wide: every LDS wave of the slice's workgroups
+      // claims from one counter, so a workgroup that has fallen behind (1-3 of a slice's 32
+      // end 40-160 us after the others, different ones every launch) is left fewer tasks, and
+      // none of a phase the others have already emptied -- then it skips the fill as well.
+      gdyn = wgdyn && A.gcnt != nullptr && gi >= A.dyn0;
+      if (gdyn && threadIdx.x == 0)
+        skipf[gi & 1u] = __hip_atomic_load(&A.gcnt[j * GCNT + gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= te - tb ? 1u : 0u;
+      block_barrier();  // every wave is done with the previous block (and sees the flag)
+      const bool skip = gdyn && skipf[gi & 1u] != 0u;
+      if (skip) te = tb;
       if (te > tb) {
         // LDS-DMA fill: one global_load_lds_dwordx4 moves 1 KiB (128 entries) per wave
         // instruction straight into LDS (no registers); H is even and hb 16-byte aligned
@@ -714,7 +737,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
         if (threadIdx.x == 0) hot[A.H] = 0.0;  // the padding column
       }
       if (threadIdx.x == 0) task_cnt = 0;  // (wave 0 is an LDS wave)
-      block_barrier();
+      if (!skip) block_barrier();
     }
     uint64_t* stp = STAMPS ? A.stamps + (static_cast<uint64_t>(blockIdx.x) * nph + gi) * 17u : nullptr;
     if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
@@ -733,12 +756,20 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       fetch(task_of(u), lt, lt ? tb : l2g0, lt ? lbase : l2base);
     };
     const uint32_t nu = nL + nR;
+    // slice-wide claims take A.dyng consecutive tasks per atomic (one address serves the whole
+    // slice: single-task claims saturate it)
+    uint32_t gcur = 0, gend = 0;
     auto claim = [&]() -> uint32_t {
+      if (gdyn && gcur < gend) return gcur++;
       uint32_t m = 0;
-      if (lane == 0) m = atomicAdd(&task_cnt, 1u);
-      return qwg + nqwg * static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
+      if (lane == 0) m = gdyn ? atomicAdd(&A.gcnt[j * GCNT + gslot], A.dyng) : atomicAdd(&task_cnt, 1u);
+      m = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
+      if (!gdyn) return qwg + nqwg * m;
+      gcur = m + 1u;
+      gend = m + A.dyng;
+      return m;
     };
-    const bool dyn = wgdyn && gi < A.nlds;
+    const bool dyn = (wgdyn && gi < A.nlds) || gdyn;
     uint32_t u = dyn ? claim() : w;
     uint32_t un = dyn ? (u < nu ? claim() : nu) : w + nw;
     if (u < nu) fetch_u(u);
@@ -958,7 +989,10 @@ __global__ __launch_bounds__(BLOCK) void k_lds_order(uint32_t c, uint64_t* out) 
 // Sum the NSHARD shards into one record and clear them for the next round (one 256-thread
 // workgroup; `out`, when given, is an LDS copy of the record for a fused finalize).
 __device__ __forceinline__ void reduce_shards_body(uint64_t* shards, uint64_t* rec, uint64_t (*part)[REC_WORDS],
-                                                   uint64_t* out) {
+                                                   uint64_t* out, uint32_t* gcnt) {
+  // (the stream launch's slice-wide task counters start the next round at zero)
+  if (gcnt)
+    for (int i = threadIdx.x; i < NSLICE * static_cast<int>(GCNT); i += BLOCK) gcnt[i] = 0;
   const int w = threadIdx.x & 31, g = threadIdx.x >> 5;
   uint64_t s = 0;
   for (int i = g * (NSHARD / 8); i < (g + 1) * (NSHARD / 8); ++i) {
@@ -976,9 +1010,9 @@ __device__ __forceinline__ void reduce_shards_body(uint64_t* shards, uint64_t* r
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void reduce_shards(uint64_t* shards, uint64_t* rec) {
+__global__ __launch_bounds__(BLOCK) void reduce_shards(uint64_t* shards, uint64_t* rec, uint32_t* gcnt) {
   __shared__ uint64_t part[8][REC_WORDS];
-  reduce_shards_body(shards, rec, part, nullptr);
+  reduce_shards_body(shards, rec, part, nullptr, gcnt);
 }
 
 // Combine the p rank records (integer sums: order-free, exact) -> next round's addthis.
@@ -1037,10 +1071,10 @@ __global__ __launch_bounds__(64) void finalize_round(const uint64_t* rec_all, in
 // p = 1: the record reduction and the finalize in one launch (one launch gap less per round).
 __global__ __launch_bounds__(BLOCK) void reduce_finalize(uint64_t* shards, uint64_t* rec, int t, uint64_t n_tot,
                                                          uint32_t extra_pages, double r0, int tracked,
-                                                         IterState* st) {
+                                                         IterState* st, uint32_t* gcnt) {
   __shared__ uint64_t part[8][REC_WORDS];
   __shared__ uint64_t tot[REC_WORDS];
-  reduce_shards_body(shards, rec, part, tot);
+  reduce_shards_body(shards, rec, part, tot, gcnt);
   __syncthreads();
   if (threadIdx.x < 64) finalize_wave(tot, 1, t, n_tot, extra_pages, r0, tracked, st);
 }
@@ -1963,7 +1997,7 @@ void dev_free(DevGraph* g) {
   F(g->x_init); F(g->xbuf[0]); F(g->xbuf[1]); F(g->r_loc[0]); F(g->r_loc[1]); F(g->r_full);
   F(g->shards); F(g->rec_local); F(g->rec_all); F(g->state); F(g->mapw);
   F(g->x_seed); F(g->r_seed);
-  F(g->dp_ell); F(g->dp_gbase); F(g->dp_out);
+  F(g->dp_ell); F(g->dp_gbase); F(g->dp_out); F(g->stream_cnt);
   const int p = g->p, rank = g->rank;
   *g = DevGraph();
   g->p = p;
@@ -2734,6 +2768,8 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   TRY(dmalloc(&g->rec_local, REC_WORDS, err));
   TRY(dmalloc(&g->rec_all, static_cast<size_t>(p) * REC_WORDS, err));
   TRY(dmalloc(&g->state, 1, err));
+  TRY(dmalloc(&g->stream_cnt, NSLICE * GCNT, err));
+  HIPTRY(hipMemsetAsync(g->stream_cnt, 0, 4ull * NSLICE * GCNT, s));
   HIPTRY(hipMemsetAsync(g->shards, 0, 8ull * NSHARD * REC_WORDS, s));
   HIPTRY(hipMemsetAsync(g->r_loc[0], 0, 8ull * (lrows ? lrows : 1), s));
   HIPTRY(hipMemsetAsync(g->r_loc[1], 0, 8ull * (lrows ? lrows : 1), s));
@@ -2756,6 +2792,7 @@ int dev_reset_state(DevGraph* g, hipStream_t s) {
   }
   HIPTRY(hipMemcpyAsync(g->state, &st, sizeof(st), hipMemcpyHostToDevice, s));
   HIPTRY(hipMemsetAsync(g->shards, 0, 8ull * NSHARD * REC_WORDS, s));
+  if (g->stream_cnt) HIPTRY(hipMemsetAsync(g->stream_cnt, 0, 4ull * NSLICE * GCNT, s));
   return PR_OK;
 }
 
@@ -2779,10 +2816,11 @@ namespace {
 constexpr int SS_MAX_DEV = 64;
 void* g_scratch_ptr[SS_MAX_DEV] = {nullptr};
 
-__global__ void k_state_set(IterState* st, IterState v, uint64_t* shards, uint32_t nwords) {
+__global__ void k_state_set(IterState* st, IterState v, uint64_t* shards, uint32_t nwords, uint32_t* gcnt) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *st = v;
   if (i < nwords) shards[i] = 0;
+  if (gcnt && i < NSLICE * GCNT) gcnt[i] = 0;
 }
 }  // namespace
 
@@ -2817,7 +2855,7 @@ int dev_reset_state_kernel(DevGraph* g, hipStream_t s) {
     st.dcnt = g->W0;
   }
   const uint32_t nw = NSHARD * REC_WORDS;
-  hipLaunchKernelGGL(k_state_set, dim3((nw + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, g->state, st, g->shards, nw);
+  hipLaunchKernelGGL(k_state_set, dim3((nw + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, g->state, st, g->shards, nw, g->stream_cnt);
   HIPTRY(hipGetLastError());
   return PR_OK;
 }
@@ -2928,6 +2966,13 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0, int part
   S.l2w = static_cast<uint32_t>(g->tune.l2w);
   S.wgdyn = static_cast<uint32_t>(env_int("PR_WGDYN", 1) != 0);
   S.l2late = static_cast<uint32_t>(g->tune.l2late);
+  S.gcnt = g->stream_cnt;
+  S.l2dyn = static_cast<uint32_t>(env_int("PR_DYNL2", g->tune.dynl2) != 0);
+  S.dyng = static_cast<uint32_t>(std::max(1, std::min(64, env_int("PR_DYNG", g->tune.dyng))));
+  {  // PR_DYNTAIL: percent of the LDS phases that keep fixed shares (100 = every phase)
+    const int pct = std::max(0, std::min(100, env_int("PR_DYNTAIL", g->tune.dyntail)));
+    S.dyn0 = pct >= 100 ? 0xFFFFFFFFu : (g->nlds * static_cast<uint32_t>(pct) + 99u) / 100u;
+  }
   S.part = static_cast<uint32_t>(part);
   // A cut launch: part 1 = the first LDS phases + the L2-hot-range tasks, part 2 = the other
   // phases + the cold-segment tasks, so both parts keep LDS-bound and L2-bound work side by
@@ -3008,6 +3053,19 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0, int part
       const uint64_t l2_t = g->gtask[j * ngs + g->nlds + 1] - g->gtask[j * ngs + g->nlds];
       fprintf(stderr, "[stamps] slice %d: lds tasks %7llu l2 tasks %7llu  workgroup end min %8.1f avg %8.1f max %8.1f us\n",
               j, (unsigned long long)lds_t, (unsigned long long)l2_t, e_min, e_avg / std::max(cnt, 1), e_max);
+      if (getenv("PR_STAMPS_WG")) {  // every workgroup of the slice: end of its LDS role / L2 role
+        fprintf(stderr, "[stamps] slice %d workgroup ends (lds role | l2 role):", j);
+        for (uint32_t b = static_cast<uint32_t>(j); b < nwg; b += NSLICE) {
+          uint64_t el = 0, e2 = 0;
+          for (uint32_t gi = 0; gi < nph; ++gi)
+            for (int w = 1; w <= 16; ++w) {
+              const uint64_t v = hst[(static_cast<size_t>(b) * nph + gi) * 17 + w];
+              if (gi == g->nlds) e2 = std::max(e2, v); else el = std::max(el, v);
+            }
+          fprintf(stderr, " %.0f|%.0f", el ? (el - t0) * 0.01 : 0.0, e2 ? (e2 - t0) * 0.01 : 0.0);
+        }
+        fprintf(stderr, "\n");
+      }
     }
   }
   HIPTRY(hipGetLastError());
@@ -3066,7 +3124,7 @@ int dev_round_rows(DevGraph* g, int t, int mode, uint32_t b0, uint32_t b1, hipSt
 int dev_round_reduce(DevGraph* g, hipStream_t s, hipEvent_t ev1) {
   std::string* err = nullptr;
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
-  hipLaunchKernelGGL(reduce_shards, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local);
+  hipLaunchKernelGGL(reduce_shards, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local, g->stream_cnt);
   HIPTRY(hipGetLastError());
   return PR_OK;
 }
@@ -3118,7 +3176,7 @@ int dev_round_single(DevGraph* g, int t, int mode, bool tracked, hipStream_t s, 
   if (ev1) HIPTRY(hipEventRecord(ev1, s));
   const uint32_t extra = (t == 1 && !g->seeded) ? g->n - g->R : 0u;  // as dev_round_finalize
   hipLaunchKernelGGL(reduce_finalize, dim3(1), dim3(BLOCK), 0, s, g->shards, g->rec_local, t, g->n_tot, extra,
-                     g->r0, tracked ? 1 : 0, g->state);
+                     g->r0, tracked ? 1 : 0, g->state, g->stream_cnt);
   HIPTRY(hipGetLastError());
   return PR_OK;
 }

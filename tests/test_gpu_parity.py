@@ -258,6 +258,40 @@ def test_sparse_exchange_bit_identical(P, O, monkeypatch, p, tiny):
     parity.assert_ranks_close(out[1], O.Graph.from_rmat(16, 16, 37).run(9)["ranks"])
 
 
+@pytest.mark.parametrize("p,tiny,dyn", [(1, False, ("0", "8", "1")), (1, True, ("30", "3", "1")),
+                                        (1, True, ("0", "1", "0")), (2, True, ("50", "2", "1")),
+                                        (4, False, ("30", "8", "1"))])
+def test_dynamic_task_claims_bit_identical(P, O, monkeypatch, p, tiny, dyn):
+    """Which wave runs a task is decided at run time in the late LDS phases and (PR_DYNL2) for
+    the L2 group -- slice-wide counters instead of fixed shares (PR_DYNTAIL percent of the
+    phases stay fixed, PR_DYNG tasks per claim).  A task's pieces and their places do not depend
+    on who runs it: ranks bit-identical to fixed shares, and the oracle's."""
+    if tiny:
+        for k, v in (("PR_HOTLDS", "256"), ("PR_NLDS", "6"), ("PR_QH", "1024"), ("PR_SEG", "512")):
+            monkeypatch.setenv(k, v)
+    scale = 16 if tiny else 20
+    out = []
+    for tail, g, l2 in (("100", "4", "0"), dyn):
+        monkeypatch.setenv("PR_DYNTAIL", tail)
+        monkeypatch.setenv("PR_DYNG", g)
+        monkeypatch.setenv("PR_DYNL2", l2)
+        if p == 1:
+            eng = P.Engine()
+            eng.generate_rmat(scale, 16, 47)
+            eng.run(7)
+            eng.run(7)               # a second run: the counters start from zero again
+            out.append(eng.ranks())
+            eng.close()
+        else:
+            grp = P.LocalGroup(p)
+            grp.each("generate_rmat", scale, 16, 47)
+            grp.run(7)
+            out.append(grp.members[0].ranks())
+            grp.close()
+    assert np.array_equal(out[0].view(np.uint64), out[1].view(np.uint64))
+    parity.assert_ranks_close(out[1], O.Graph.from_rmat(scale, 16, 47).run(7)["ranks"])
+
+
 @pytest.mark.parametrize("p,scale,ef", [(8, 9, 2), (5, 11, 4), (7, 12, 8), (6, 8, 1)])
 def test_sparse_exchange_small_graphs(P, O, p, scale, ef):
     """Sparse exchange corner cases: many (chunk, peer) lists empty (tiny graphs at 8 ranks),
