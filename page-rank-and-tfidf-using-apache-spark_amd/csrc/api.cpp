@@ -1170,8 +1170,9 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       // launch runs in chunks of class-A row blocks; as chunk k's x' slot pieces are final,
       // the comm stream sends them to every peer (grouped ncclSend/ncclRecv over xGMI, one
       // direct link per peer) while the compute stream runs the next chunk.  The exact
-      // records are all-gathered after the last rows, finalize runs on the comm stream, and
-      // the next round's stream launch waits for it.
+      // records are all-gathered after the last rows and finalize runs on the comm stream.
+      // The next round's stream launch waits for all of that, or (overlapped, want_overlap)
+      // its first part only for chunk 0.
       double* xf = prmi::dev_x_out(g, t);
       if (ov) {
         // part 1 needs chunk 0 of the last round only; part 2 and the rows need the rest of

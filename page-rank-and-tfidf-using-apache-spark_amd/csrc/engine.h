@@ -103,7 +103,7 @@ struct Tuning {
                         // workgroups in fixed shares; the later phases are claimed slice-wide
   int dyng = 4;         // PR_DYNG: tasks per slice-wide claim
   int dynl2 = 0;        // PR_DYNL2: the L2-role waves claim their tasks slice-wide too
-  int stream_cus = 32;  // PR_STREAM_CUS: stream workgroups (= compute units) per XCD
+  int stream_cus = 32;  // PR_STREAM_CUS: stream workgroups (= compute units) per XCD; 31 at p > 1
   int l2late = 0;       // PR_L2LATE: L2-role waves prefetch the next task's columns after
                         // their gathers instead of before (see StreamArgs::l2late)
   int lean = 1;         // PR_LEAN: 1 = the lean per-task instruction stream of the stream launch

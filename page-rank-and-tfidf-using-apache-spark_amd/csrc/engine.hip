@@ -2081,7 +2081,11 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.l2mode = env_int("PR_L2MODE", T.l2mode);
   T.l2w = std::max(0, std::min(12, env_int("PR_L2W", T.l2w)));
   T.l2late = env_int("PR_L2LATE", T.l2late);
-  T.stream_cus = env_int("PR_STREAM_CUS", T.stream_cus);
+  // p > 1: the stream launch leaves one compute unit of every XCD free.  Its workgroups hold a
+  // compute unit's whole LDS for the length of the launch, so nothing else can start beside
+  // them -- and with the overlapped exchange RCCL's send/recv kernels must run beside part 1 of
+  // the launch, or the chunks behind the hot prefix only travel once it has ended.
+  T.stream_cus = env_int("PR_STREAM_CUS", p > 1 ? 31 : T.stream_cus);
   T.dpull = static_cast<uint32_t>(std::max(0, env_int("PR_DPULL", 0)));
   T.dropdeg = static_cast<uint32_t>(std::max(0, env_int("PR_DROPDEG", 0)));
   T.keepdeg = static_cast<uint32_t>(std::max(0, env_int("PR_KEEPDEG", 0)));
