@@ -3004,7 +3004,7 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0, int part
     HIPTRY(hipMemcpyAsync(hst.data(), dst, 8 * hst.size(), hipMemcpyDeviceToHost, s));
     HIPTRY(hipStreamSynchronize(s));
     (void)hipFree(dst);
-    const uint32_t nwg = NSLICE * 32;
+    const uint32_t nwg = NSLICE * static_cast<uint32_t>(std::max(1, std::min(32, g->tune.stream_cus)));
     double prev_end = 0;
     uint64_t t0 = ~0ull;
     for (uint32_t b = 0; b < nwg; ++b) t0 = std::min<uint64_t>(t0, hst[(static_cast<size_t>(b) * nph) * 17]);
