@@ -101,6 +101,7 @@ struct Tuning {
   uint32_t keepdeg = 0; // PR_KEEPDEG: rows at or above this in-degree leave the streams (timing only)
   int dyntail = 100;    // PR_DYNTAIL: percent of the LDS phases whose tasks go to the slice's
                         // workgroups in fixed shares; the later phases are claimed slice-wide
+  int early = 0;        // PR_EARLY: LDS waves claim and fetch a phase's first task before its barrier
   int dyng = 4;         // PR_DYNG: tasks per slice-wide claim
   int dynl2 = 0;        // PR_DYNL2: the L2-role waves claim their tasks slice-wide too
   int stream_cus = 32;  // PR_STREAM_CUS: stream workgroups (= compute units) per XCD; 31 at p > 1

@@ -410,6 +410,7 @@ struct StreamArgs {
   uint32_t wgdyn;            // PR_WGDYN: LDS waves claim their workgroup's tasks from an LDS
                              // counter (1) or take them round-robin (0)
   uint32_t* gcnt;            // [NSLICE * GCNT] task counters of the slice-wide claims (zero at launch)
+  uint32_t early;            // PR_EARLY: first task of a phase claimed and fetched before its barrier
   uint32_t dyng;             // tasks per slice-wide claim (PR_DYNG)
   uint32_t l2dyn;            // PR_DYNL2: the L2-role waves claim their tasks slice-wide as well
   uint32_t dyn0;             // LDS phases >= dyn0 deal their tasks to the slice's workgroups from
@@ -617,14 +618,19 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // with split roles, a phase's LDS tasks are dealt to the slice's workgroups round-robin
   // (task u to workgroup u mod 32) and the workgroup's LDS waves claim its tasks from this
   // counter, so no wave idles at the phase barrier while a sibling still has a backlog
-  uint32_t& task_cnt = *reinterpret_cast<uint32_t*>(hot + A.H + 2);
+  // (two counters, one per phase parity: a wave that is done with phase gi may claim its first
+  // tasks of phase gi + 1 -- and start fetching their columns -- before the phase barrier)
+  uint32_t* tcnt = reinterpret_cast<uint32_t*>(hot + A.H + 2);
   // slice-wide claims: "this phase has no task left" flags, one per phase parity
   uint32_t* skipf = reinterpret_cast<uint32_t*>(hot + A.H + 3);
   const bool wgdyn = split && !l2role && A.wgdyn != 0u;
   const uint32_t qwg = blockIdx.x / NSLICE, nqwg = gridDim.x / NSLICE;
   uint32_t bar_gen = 0;
   if (split) {
-    if (threadIdx.x == 0) bar_cnt = 0;
+    if (threadIdx.x == 0) {
+      bar_cnt = 0;
+      tcnt[0] = tcnt[1] = 0;
+    }
     __syncthreads();
   }
   auto block_barrier = [&]() {
@@ -700,7 +706,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   for (uint32_t gi = g0; gi < g1; ++gi) {
     uint32_t tb = l2b, te = l2b, rb = l2b, re = l2e;  // LDS-block tasks, L2 share
     uint64_t lbase = 0;
-    bool gdyn = false;
+    bool gdyn = false, lds_phase = false;
     uint32_t gslot = gi;  // counter of this phase's slice-wide claims
     if (onlyl2 || (gi == A.nlds && (l2last || l2role))) {
       // the L2 phase / role: no LDS block, the whole L2 group (segments swept in order); with
@@ -708,18 +714,23 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       gdyn = l2role && A.l2dyn != 0u && A.gcnt != nullptr;
       gslot = A.part == 2u ? 65u : 64u;
     } else if (A.nlds) {
+      lds_phase = true;
       tb = A.gtask[j * ngs + gi];
       te = A.gtask[j * ngs + gi + 1];
       lbase = A.gbase[j * ngs + gi];
       rb = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * gi) / A.nlds);
       re = l2b + static_cast<uint32_t>((static_cast<uint64_t>(l2e - l2b) * (gi + 1)) / A.nlds);
       if (l2last || split) rb = re = l2b;
-      const uint32_t hb = A.hot_base[j] + gi * A.H;
-      // Late phases deal their tasks slice-wide: every LDS wave of the slice's workgroups
-      // claims from one counter, so a workgroup that has fallen behind (1-3 of a slice's 32
-      // end 40-160 us after the others, different ones every launch) is left fewer tasks, and
-      // none of a phase the others have already emptied -- then it skips the fill as well.
+      // Late phases may deal their tasks slice-wide (PR_DYNTAIL): every LDS wave of the slice's
+      // workgroups claims from one counter, so a workgroup that has fallen behind (1-3 of a
+      // slice's 32 end 40-160 us after the others, different ones every launch) is left fewer
+      // tasks, and none of a phase the others have already emptied -- then it skips the fill.
       gdyn = wgdyn && A.gcnt != nullptr && gi >= A.dyn0;
+    }
+    // entering an LDS phase: barrier (every wave is done with the previous block), fill, reset
+    // of the other parity's task counter, barrier
+    auto enter_phase = [&]() {
+      const uint32_t hb = A.hot_base[j] + gi * A.H;
       if (gdyn && threadIdx.x == 0)
         skipf[gi & 1u] = __hip_atomic_load(&A.gcnt[j * GCNT + gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= te - tb ? 1u : 0u;
       block_barrier();  // every wave is done with the previous block (and sees the flag)
@@ -733,14 +744,19 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
           const uint32_t e0 = q * 128u + 2u * static_cast<uint32_t>(lane);
           if (e0 < A.H) __builtin_amdgcn_global_load_lds(x + hb + e0, hot + q * 128u, 16, 0, 0);
         }
+        // (vmcnt counts in order: the wait also covers column words fetched ahead of the fill)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (threadIdx.x == 0) hot[A.H] = 0.0;  // the padding column
       }
-      if (threadIdx.x == 0) task_cnt = 0;  // (wave 0 is an LDS wave)
+      if (threadIdx.x == 0) tcnt[(gi + 1u) & 1u] = 0;  // (wave 0 is an LDS wave)
       if (!skip) block_barrier();
-    }
+    };
+    // PR_EARLY: with workgroup-local claims a wave claims its first tasks of the phase and
+    // fetches the first one's column words before it enters the phase, so that fetch's HBM
+    // latency passes during the barrier and the fill instead of after them
+    const bool early = lds_phase && wgdyn && !gdyn && A.early != 0u;
+    if (lds_phase && !early) enter_phase();
     uint64_t* stp = STAMPS ? A.stamps + (static_cast<uint64_t>(blockIdx.x) * nph + gi) * 17u : nullptr;
-    if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
     const uint32_t nL = te - tb, nR = re - rb, nm = min(nL, nR);
     // virtual index u -> task: alternate LDS / L2 tasks while both last, then the rest
     auto is_lds = [&](uint32_t u) -> bool {
@@ -762,7 +778,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     auto claim = [&]() -> uint32_t {
       if (gdyn && gcur < gend) return gcur++;
       uint32_t m = 0;
-      if (lane == 0) m = gdyn ? atomicAdd(&A.gcnt[j * GCNT + gslot], A.dyng) : atomicAdd(&task_cnt, 1u);
+      if (lane == 0) m = gdyn ? atomicAdd(&A.gcnt[j * GCNT + gslot], A.dyng) : atomicAdd(&tcnt[gi & 1u], 1u);
       m = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
       if (!gdyn) return qwg + nqwg * m;
       gcur = m + 1u;
@@ -773,6 +789,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     uint32_t u = dyn ? claim() : w;
     uint32_t un = dyn ? (u < nu ? claim() : nu) : w + nw;
     if (u < nu) fetch_u(u);
+    if (early) enter_phase();
+    if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
     while (u < nu) {
       const bool lds_task = is_lds(u);
       u32x4 cv[4];
@@ -2298,14 +2316,15 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
       // measured optimum on one rank is 1 / 3 / 8 / 20 / 52-64 blocks at R-MAT scale 20 / 22 /
       // 24 / 26 / 28 (B = 3.5 / 13 / 46 / 168 / 610), i.e. 0.41 B^0.77: the hot share worth an
       // LDS fill shrinks slowly as the graph grows (23 % of a slice's columns at scale 22, 9 %
-      // at scale 28).  A fixed 20 cost 25 % at scale 22 and 13 % at scale 28.  A rank of p >= 2
-      // takes 0.75 x (p = 2) or 0.6 x (p >= 4) of that: its share of every phase shrinks with
-      // p while the per-phase cost stays (scale 26: 15 and 12; scale 28 at 8 ranks: 40 against
-      // 24 and 12).  Cold segments widen until the row launch's stream table holds every
-      // (slice, segment).
+      // at scale 28).  A fixed 20 cost 25 % at scale 22 and 13 % at scale 28.  A rank of p >= 4
+      // takes 0.6 x that: its share of every phase shrinks with p while the per-phase cost
+      // stays (scale 26 at 8 ranks: flat from 10 to 15 blocks, 6 and 8 lose 3-7 %; at 4 ranks
+      // flat from 12 to 20; scale 28 at 8 ranks: 34 against 12); two ranks keep the single-rank
+      // count (scale 26: 19-24 blocks 2.81-2.90 ms for both shares, 15 blocks 3.02, 11 2.95).
+      // Cold segments widen until the row launch's stream table holds every (slice, segment).
       int want = nlds_env;
       if (want < 0) {
-        const double f = p >= 4 ? 0.6 : (p >= 2 ? 0.75 : 1.0);
+        const double f = p >= 4 ? 0.6 : 1.0;
         want = static_cast<int>(0.41 * f * std::pow(static_cast<double>(g->SL) / G.H, 0.77) + 0.5);
         want = std::max(1, want);
       }
@@ -2972,6 +2991,7 @@ int dev_round_stream(DevGraph* g, int t, hipStream_t s, hipEvent_t ev0, int part
   S.l2late = static_cast<uint32_t>(g->tune.l2late);
   S.gcnt = g->stream_cnt;
   S.l2dyn = static_cast<uint32_t>(env_int("PR_DYNL2", g->tune.dynl2) != 0);
+  S.early = static_cast<uint32_t>(env_int("PR_EARLY", g->tune.early) != 0);
   S.dyng = static_cast<uint32_t>(std::max(1, std::min(64, env_int("PR_DYNG", g->tune.dyng))));
   {  // PR_DYNTAIL: percent of the LDS phases that keep fixed shares (100 = every phase)
     const int pct = std::max(0, std::min(100, env_int("PR_DYNTAIL", g->tune.dyntail)));
