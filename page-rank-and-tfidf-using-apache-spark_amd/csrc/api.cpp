@@ -50,6 +50,7 @@ struct pr_ctx {
   // multi-rank exchange: a comm stream beside the compute stream, chunk events
   hipStream_t comm_stream = nullptr;
   std::vector<hipEvent_t> ev_chunk;
+  std::vector<hipEvent_t> ev_pack;  // rank group: chunk k of this member's send buffer is packed
   hipEvent_t ev_rec = nullptr, ev_done = nullptr;
   hipEvent_t ev_x0 = nullptr;     // chunk 0 of this round's x' (the hot prefix) has landed here
   int xchunks = 4;                // PR_XCHUNKS: row-launch chunks of the x' exchange
@@ -120,6 +121,17 @@ bool want_sx(const pr_ctx* c) {
   int v = 1;
   if (const char* e = getenv("PR_SPARSE_X")) v = atoi(e);
   return c->opts.n_ranks > 1 && v != 0;
+}
+
+// Where the sparse exchange packs a chunk's send buffers (PR_PACKCOMM: 1 = on the comm stream,
+// the default; 0 = on the compute stream behind the chunk's rows).  The packs are four short
+// launches per round (48 us per rank at 8 ranks, scale 26, against 0.17 ms of row launches);
+// only the sends need them, so they run ahead of each chunk's sends and the compute stream goes
+// straight on to the next chunk's rows.
+bool pack_on_comm() {
+  int v = 1;
+  if (const char* e = getenv("PR_PACKCOMM")) v = atoi(e);
+  return v != 0;
 }
 
 // Overlapped exchange (PR_XOVERLAP: 1 = on, the default; 0 = the round-2 schedule): the next
@@ -557,6 +569,7 @@ void pr_destroy(pr_ctx* c) {
     prmi::dev_free(&c->dg);
     for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_chunk) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_pack) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->prog_ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ext_kev) (void)hipEventDestroy(e);
     if (c->ev_rec) (void)hipEventDestroy(c->ev_rec);
@@ -677,12 +690,18 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       HIPCHK(c0, hipEventCreateWithFlags(&e, hipEventDisableTiming));
       m->ev_chunk.push_back(e);
     }
+    while (m->ev_pack.size() < plans[i].size()) {
+      hipEvent_t e;
+      HIPCHK(c0, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      m->ev_pack.push_back(e);
+    }
   }
   for (int i = 1; i < n; ++i)
     if (plans[i].size() != plans[0].size()) return fail(c0, PR_E_ARG, "local group: exchange plans differ");
   // sparse exchange: every member's lists, and rank r's send counts to q equal q's receive
   // counts from r for every chunk (the lists of pr_run's RCCL path, checked here on the host)
   const bool sx = n > 1 && want_sx(c0);
+  const bool pkc = sx && pack_on_comm();
   if (sx) {
     for (int i = 0; i < n; ++i) {
       HIPCHK(c0, hipSetDevice(ctxs[i]->device));
@@ -722,7 +741,7 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       }
       for (size_t k = 0; !rc && k < plans[i].size(); ++k) {
         rc = prmi::dev_round_rows(&m->dg, t, mode, plans[i][k].b0, plans[i][k].b1, m->stream);
-        if (!rc && sx) rc = prmi::dev_sx_pack(&m->dg, t, static_cast<int>(k), m->stream);
+        if (!rc && sx && !pkc) rc = prmi::dev_sx_pack(&m->dg, t, static_cast<int>(k), m->stream);
         if (!rc && hipEventRecord(m->ev_chunk[k], m->stream) != hipSuccess) rc = PR_E_HIP;
       }
       if (!rc) rc = prmi::dev_round_rows(&m->dg, t, mode, m->dg.nb_rows_a, m->dg.nb_rows, m->stream);
@@ -730,21 +749,34 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
       if (rc) return fail(c0, rc, "round compute");
       HIPCHK(c0, hipEventRecord(m->ev_rec, m->stream));
     }
-    for (int q = 0; q < n; ++q) {
-      pr_ctx* mq = ctxs[q];
-      DevGraph* dst = &mq->dg;
-      HIPCHK(c0, hipSetDevice(mq->device));
-      for (size_t k = 0; k < plans[q].size(); ++k) {
+    // chunk by chunk, as on a rank's comm stream under RCCL: pack (the sender's comm stream),
+    // the copies that stand for send / recv, unpack (the receiver's)
+    for (size_t k = 0; k < plans[0].size(); ++k) {
+      if (pkc)
+        for (int r = 0; r < n; ++r) {
+          pr_ctx* mr = ctxs[r];
+          HIPCHK(c0, hipSetDevice(mr->device));
+          HIPCHK(c0, hipStreamWaitEvent(mr->comm_stream, mr->ev_chunk[k], 0));
+          int rcp = prmi::dev_sx_pack(&mr->dg, t, static_cast<int>(k), mr->comm_stream);
+          if (rcp) return fail(c0, rcp, "sparse exchange pack");
+          HIPCHK(c0, hipEventRecord(mr->ev_pack[k], mr->comm_stream));
+        }
+      for (int q = 0; q < n; ++q) {
+        pr_ctx* mq = ctxs[q];
+        DevGraph* dst = &mq->dg;
+        HIPCHK(c0, hipSetDevice(mq->device));
+        // (the event behind which member r's chunk k may be read)
+        auto ready = [&](int r) { return pkc ? ctxs[r]->ev_pack[k] : ctxs[r]->ev_chunk[k]; };
         if (xdelay) {
           for (int r = 0; r < n; ++r)
-            if (r != q) HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ctxs[r]->ev_chunk[k], 0));
+            if (r != q) HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ready(r), 0));
           int rcd = prmi::dev_delay_us(xdelay, mq->comm_stream);
           if (rcd) return fail(c0, rcd, "delay kernel");
         }
         for (int r = 0; r < n; ++r) {
           if (r == q) continue;
           DevGraph* src = &ctxs[r]->dg;
-          HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ctxs[r]->ev_chunk[k], 0));
+          HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ready(r), 0));
           if (sx) {  // r's packed entries for q -> q's receive buffer, as ncclSend / ncclRecv
             const size_t is = k * n + q, ir = k * n + r;
             const uint64_t cnt = src->sx_so[is + 1] - src->sx_so[is];
@@ -766,6 +798,11 @@ int pr_run_group(pr_ctx** ctxs, int32_t n, int32_t iterations, double tol, pr_st
         }
         if (k == 0) HIPCHK(c0, hipEventRecord(mq->ev_x0, mq->comm_stream));
       }
+    }
+    for (int q = 0; q < n; ++q) {
+      pr_ctx* mq = ctxs[q];
+      DevGraph* dst = &mq->dg;
+      HIPCHK(c0, hipSetDevice(mq->device));
       for (int r = 0; r < n; ++r) {
         DevGraph* src = &ctxs[r]->dg;
         HIPCHK(c0, hipStreamWaitEvent(mq->comm_stream, ctxs[r]->ev_rec, 0));
@@ -1136,6 +1173,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
   std::vector<prmi::XChunk> plan;
   bool sx = false;  // sparse x' exchange this run
   const bool ov = want_overlap(c, tol);
+  const bool pkc = pack_on_comm();
   if (p > 1) {  // (before ev_start: list building and its collectives are set-up, not rounds)
     rc = ensure_xchg(c);
     if (rc) return rc;
@@ -1189,7 +1227,7 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       if (rc) return fail(c, rc, "round compute");
       for (size_t k = 0; k < plan.size(); ++k) {
         rc = prmi::dev_round_rows(g, t, mode, plan[k].b0, plan[k].b1, c->stream);
-        if (!rc && sx) rc = prmi::dev_sx_pack(g, t, static_cast<int>(k), c->stream);
+        if (!rc && sx && !pkc) rc = prmi::dev_sx_pack(g, t, static_cast<int>(k), c->stream);
         if (rc) return fail(c, rc, "round rows");
         HIPCHK(c, hipEventRecord(c->ev_chunk[k], c->stream));
       }
@@ -1199,6 +1237,10 @@ int pr_run(pr_ctx* c, int32_t iterations, double tol, pr_stats* st) {
       HIPCHK(c, hipEventRecord(c->ev_rec, c->stream));
       for (size_t k = 0; k < plan.size(); ++k) {
         HIPCHK(c, hipStreamWaitEvent(c->comm_stream, c->ev_chunk[k], 0));
+        if (sx && pkc) {
+          rc = prmi::dev_sx_pack(g, t, static_cast<int>(k), c->comm_stream);
+          if (rc) return fail(c, rc, "sparse exchange pack");
+        }
         NCCLCHK(c, ncclGroupStart());
         if (sx) {  // the packed entries each peer references (counts agreed in sx_setup_rccl)
           for (int q = 0; q < p; ++q) {

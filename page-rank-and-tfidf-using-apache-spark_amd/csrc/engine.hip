@@ -2088,11 +2088,8 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   T.heavy_deg = static_cast<uint32_t>(std::max(0, env_int("PR_HDEG", static_cast<int>(T.heavy_deg))));
   T.rb = static_cast<uint32_t>(std::max(64, std::min(RB, env_int("PR_RB", static_cast<int>(T.rb)))));
   T.rxg = static_cast<uint32_t>(std::max(1, std::min(4096, env_int("PR_RXG", static_cast<int>(T.rxg)))));
-  // a rank's share of each (slice, LDS block) phase shrinks with p while the per-phase cost
-  // (block fill, phase tail) stays: fewer blocks per slice at p > 1 (measured per-rank SpMV
-  // at scale 26: p = 2 best at 15, p = 4 and 8 at 12; profiles/r01/multirank/)
-  // PR_NLDS overrides; otherwise the count follows the graph (below, once the slice length is
-  // known)
+  // LDS blocks per slice: PR_NLDS overrides; otherwise the count follows the graph and the
+  // rank count (below, once the slice length is known)
   const int nlds_env = env_int("PR_NLDS", -1);
   T.stream_wg = std::max(1, std::min(2, env_int("PR_STREAM_WG", T.stream_wg)));
   if (const char* cm = getenv("PR_COLMASK")) T.colmask = static_cast<uint32_t>(strtoul(cm, nullptr, 0));

@@ -57,6 +57,26 @@ def test_overlapped_schedule_bit_identical(P, O, monkeypatch, p, tiny, sx, delay
     parity.assert_ranks_close(out[1], O.Graph.from_rmat(scale, 16, 43).run(8)["ranks"])
 
 
+@pytest.mark.parametrize("p,tiny,delay", [(4, True, 0), (8, False, 0), (2, True, 200)])
+def test_pack_stream_bit_identical(P, monkeypatch, p, tiny, delay):
+    """The sparse exchange packs a chunk's send buffers on the comm stream, ahead of the chunk's
+    sends (PR_PACKCOMM=1, the default), or on the compute stream behind the chunk's rows (0):
+    the same ranks, bit for bit, with and without the overlapped schedule."""
+    if tiny:
+        for k, v in TINY:
+            monkeypatch.setenv(k, v)
+    if delay:
+        monkeypatch.setenv("PR_XDELAY_US", str(delay))
+    scale = 16 if tiny else 19
+    out = []
+    for pk, ov in (("0", "1"), ("1", "1"), ("1", "0")):
+        monkeypatch.setenv("PR_PACKCOMM", pk)
+        monkeypatch.setenv("PR_XOVERLAP", ov)
+        out.append(group_ranks(P, p, scale, 16, 47, 8)[0])
+    assert np.array_equal(out[0].view(np.uint64), out[1].view(np.uint64))
+    assert np.array_equal(out[0].view(np.uint64), out[2].view(np.uint64))
+
+
 def test_overlapped_schedule_tracked_and_crash_round(P, O, monkeypatch):
     """Tracked mode (exact residual and rank sum through the overlapped rounds) and the round of
     the empty-collection crash (PageRank.java:125) are those of the uncut schedule."""
