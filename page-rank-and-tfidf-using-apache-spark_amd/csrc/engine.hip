@@ -591,10 +591,17 @@ __device__ __forceinline__ void gather16(double (&v)[EPL], const uint32_t (&qo)[
 // NT: 2 = non-temporal piece stores.  SPLIT: dedicated L2 waves (A.l2w).  STAMPS: PR_STAMPS
 // diagnostics.  The variants are separate instantiations so that the default one carries no
 // register cost for the others.
-// EXP: the A/B switches of round 3 each live in an instantiation of their own (1 = PR_L2LATE=1,
-// 2 = PR_L2LATE=2, 4 = PR_DBG=8192); together inside the default one they cost 12 VGPRs and
-// pushed its hot loop into scratch spills (1.65 -> 1.99 ms per launch).
-template <int NT, bool SPLIT, bool STAMPS, int NTC = 0, bool LEAN = false, int EXP = 0>
+// EXP: a bit mask of what the instantiation carries beyond the plain launch.  The A/B switches
+// each live in an instantiation of their own (1 = PR_L2LATE=1, 2 = PR_L2LATE=2, 4 = PR_DBG=8192):
+// together inside the default one they cost 12 VGPRs and pushed its hot loop into scratch spills
+// (1.65 -> 1.99 ms per launch).  So do the features a single rank's plain launch never uses
+// (8 = slice-wide task claims, 16 = early first-task fetch, 32 = the cut launch of the overlapped
+// exchange): compiled into the default instantiation their wave-uniform state doubled its SGPR
+// spills (25 -> 47 registers kept in VGPR lanes, read back inside the task loop) and cost the
+// stream launch 6 % (1.67 -> 1.78 ms).  The default of the template parameter is "everything"
+// for the older variants; the shipped lean kernel is instantiated with 0, 32 and 56.
+constexpr int EXP_ALL = 8 | 16 | 32;
+template <int NT, bool SPLIT, bool STAMPS, int NTC = 0, bool LEAN = false, int EXP = EXP_ALL>
 __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   extern __shared__ __attribute__((aligned(16))) double hot[];
   const uint32_t j = blockIdx.x % NSLICE;
@@ -605,7 +612,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // (gathers through the XCD's L2) for the whole launch while the other LW waves run the LDS
   // phases: latency-bound gathers beside bandwidth-bound LDS tasks.  The LW waves then sync
   // with an LDS-counter barrier of their own (the L2 waves never wait).
-  const bool onlyl2 = A.part == 2u && A.ph_lo >= A.ph_hi;
+  constexpr bool X_DYN = (EXP & 8) != 0, X_EARLY = (EXP & 16) != 0, X_PARTS = (EXP & 32) != 0;
+  const bool onlyl2 = X_PARTS && A.part == 2u && A.ph_lo >= A.ph_hi;
   const bool split = SPLIT && A.l2w != 0u && A.nlds != 0u && !onlyl2;
   const uint32_t LW = split ? wpb - A.l2w : wpb;
   const bool l2role = split && wv >= LW;
@@ -664,7 +672,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   uint32_t bnx = 0, tpn = 0;
   const uint32_t l2g = j * ngs + A.nlds;
   const uint32_t l2g0 = A.gtask[l2g];              // first task of the slice's L2 group
-  const uint32_t l2b = A.l2lo[j], l2e = A.l2hi[j];  // the part of it this launch sweeps
+  // the part of it this launch sweeps (all of it unless the launch is one part of a cut launch)
+  const uint32_t l2b = X_PARTS ? A.l2lo[j] : l2g0, l2e = X_PARTS ? A.l2hi[j] : A.gtask[l2g + 1];
   const uint64_t l2base = A.gbase[l2g];
   auto fetch = [&](uint32_t tt, bool lds_task, uint32_t gtb, uint64_t gbs) {
     // PR_DBG=2048 / 4096 (timing only, wrong sums): every LDS-group / L2-group task reads the
@@ -701,8 +710,8 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
   // LDS blocks the single phase is the whole stream.
   const bool l2last = A.l2mode == 1u && A.nlds && !split;  // one final phase for every L2 task
   const uint32_t nph = (A.nlds && !onlyl2) ? A.nlds + ((l2last || split) ? 1u : 0u) : 1u;  // (stamp slots)
-  const uint32_t g0 = l2role ? A.nlds : (split ? A.ph_lo : 0u),
-                 g1 = split ? (l2role ? A.nlds + 1u : A.ph_hi) : nph;
+  const uint32_t g0 = l2role ? A.nlds : ((split && X_PARTS) ? A.ph_lo : 0u),
+                 g1 = split ? (l2role ? A.nlds + 1u : (X_PARTS ? A.ph_hi : A.nlds)) : nph;
   for (uint32_t gi = g0; gi < g1; ++gi) {
     uint32_t tb = l2b, te = l2b, rb = l2b, re = l2e;  // LDS-block tasks, L2 share
     uint64_t lbase = 0;
@@ -711,7 +720,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     if (onlyl2 || (gi == A.nlds && (l2last || l2role))) {
       // the L2 phase / role: no LDS block, the whole L2 group (segments swept in order); with
       // l2dyn its tasks go to the slice's L2 waves in claim order, front to back
-      gdyn = l2role && A.l2dyn != 0u && A.gcnt != nullptr;
+      gdyn = X_DYN && l2role && A.l2dyn != 0u && A.gcnt != nullptr;
       gslot = A.part == 2u ? 65u : 64u;
     } else if (A.nlds) {
       lds_phase = true;
@@ -725,7 +734,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
       // workgroups claims from one counter, so a workgroup that has fallen behind (1-3 of a
       // slice's 32 end 40-160 us after the others, different ones every launch) is left fewer
       // tasks, and none of a phase the others have already emptied -- then it skips the fill.
-      gdyn = wgdyn && A.gcnt != nullptr && gi >= A.dyn0;
+      gdyn = X_DYN && wgdyn && A.gcnt != nullptr && gi >= A.dyn0;
     }
     // entering an LDS phase: barrier (every wave is done with the previous block), fill, reset
     // of the other parity's task counter, barrier
@@ -754,7 +763,7 @@ __global__ __launch_bounds__(STREAM_BLOCK) void spmv_stream(StreamArgs A) {
     // PR_EARLY: with workgroup-local claims a wave claims its first tasks of the phase and
     // fetches the first one's column words before it enters the phase, so that fetch's HBM
     // latency passes during the barrier and the fill instead of after them
-    const bool early = lds_phase && wgdyn && !gdyn && A.early != 0u;
+    const bool early = X_EARLY && lds_phase && wgdyn && !gdyn && A.early != 0u;
     if (lds_phase && !early) enter_phase();
     uint64_t* stp = STAMPS ? A.stamps + (static_cast<uint64_t>(blockIdx.x) * nph + gi) * 17u : nullptr;
     const uint32_t nL = te - tb, nR = re - rb, nm = min(nL, nR);
@@ -2920,16 +2929,21 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   const bool lean = g->tune.lean != 0;
   static bool lattr = false;
   if (!lattr) {
-    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true>),
+    for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 0>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 32>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, EXP_ALL>),
                           reinterpret_cast<const void*>(&spmv_stream<2, true, true, 0, true>),
                           reinterpret_cast<const void*>(&spmv_stream<0, true, false, 0, true>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     lattr = true;
   }
+  // what the launch needs of the kernel beyond the plain single-rank form (see EXP)
+  const bool want_dyn = A.gcnt != nullptr && (A.dyn0 < A.nlds || A.l2dyn != 0u);
+  const int feat = (want_dyn || A.early != 0u) ? EXP_ALL : (A.part != 0u ? 32 : 0);
   const int exper = g->tune.l2late == 1 ? 1 : (g->tune.l2late == 2 ? 2 : ((g->tune.dbg & (8192 | 16384)) ? 4 : 0));
   // (PR_DBG=16384 runs the PR_DBG=8192 instantiation with its fast path off: that variant
   // carries 22 spilled registers, so its A/B partner must carry them too)
-  if (exper && g->tune.nt == 2 && split && lean && !st) {
+  if (exper && !feat && g->tune.nt == 2 && split && lean && !st) {
     static bool eattr = false;
     if (!eattr) {
       for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 1>),
@@ -2946,7 +2960,9 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   if (g->tune.nt == 0 && split && lean && !st) hipLaunchKernelGGL((spmv_stream<0, true, false, 0, true>), gr, bl, lds, s, A);
   else if (g->tune.nt != 2) hipLaunchKernelGGL((spmv_stream<0, false, false>), gr, bl, lds, s, A);
   else if (split && st && lean) hipLaunchKernelGGL((spmv_stream<2, true, true, 0, true>), gr, bl, lds, s, A);
-  else if (split && lean) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true>), gr, bl, lds, s, A);
+  else if (split && lean && feat == EXP_ALL) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, EXP_ALL>), gr, bl, lds, s, A);
+  else if (split && lean && feat == 32) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, 32>), gr, bl, lds, s, A);
+  else if (split && lean) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, 0>), gr, bl, lds, s, A);
   else if (split && st) hipLaunchKernelGGL((spmv_stream<2, true, true>), gr, bl, lds, s, A);
   else if (split) hipLaunchKernelGGL((spmv_stream<2, true, false>), gr, bl, lds, s, A);
   else if (st) hipLaunchKernelGGL((spmv_stream<2, false, true>), gr, bl, lds, s, A);

@@ -4,7 +4,12 @@ The stream launch runs one 1024-thread workgroup per compute unit, so it has 128
 lane and not one more: a change that pushes the default instantiation over that line spills its
 hot loop to scratch and costs 20 % of the launch without failing any parity test.  This test
 fails instead: the default stream kernel and the three row kernels must carry no spilled
-registers and no scratch.
+registers and no scratch.  Scalar registers have the same kind of cliff: wave-uniform state
+that does not fit is kept in VGPR lanes and read back with v_readlane inside the task loop.  With
+the cut-launch, claim and early-fetch features compiled into the single-rank instantiation it
+held 47 such registers instead of 25 and the stream launch took 6 % longer, again with every
+parity test green -- so the shipped instantiations (plain, and the cut launch of the overlapped
+exchange) are bounded here as well.
 """
 import os
 import re
@@ -42,9 +47,13 @@ def kernel_notes():
 def test_default_spmv_kernels_do_not_spill(engine_mod):
     ks = kernel_notes()
     stream = [n for n in ks if "spmv_stream" in n and n.endswith("ILi2ELb1ELb0ELi0ELb1ELi0EEEvNS_10StreamArgsE")]
+    cut = [n for n in ks if "spmv_stream" in n and n.endswith("ILi2ELb1ELb0ELi0ELb1ELi32EEEvNS_10StreamArgsE")]
     rows = [n for n in ks if "spmv_rows" in n]
-    assert len(stream) == 1 and len(rows) == 3, sorted(ks)
-    for n in stream + rows:
+    assert len(stream) == 1 and len(cut) == 1 and len(rows) == 3, sorted(ks)
+    for n in stream + cut + rows:
         k = ks[n]
         assert k["vgpr_spill_count"] == 0 and k["private_segment_fixed_size"] == 0, (n, k)
         assert k["vgpr_count"] <= 128, (n, k)
+    # SGPRs kept in VGPR lanes: 26 (plain) and 31 (cut launch) when this was written
+    assert ks[stream[0]]["sgpr_spill_count"] <= 30, ks[stream[0]]
+    assert ks[cut[0]]["sgpr_spill_count"] <= 36, ks[cut[0]]
