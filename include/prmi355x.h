@@ -171,6 +171,15 @@ int pr_progress(pr_ctx* ctx, int32_t* rounds_enqueued, int32_t* rounds_done);
  * *lane_order_cases = patterns whose bits equal the serial sum in ascending lane order. */
 int pr_selftest_sum_order(pr_ctx* ctx, uint32_t cases, uint32_t launches, uint64_t* copies,
                           uint64_t* differing, uint64_t* lane_order_cases);
+
+/* Measurement aid without a counterpart in the reference: moves one of the arrays a round
+ * touches ("partial" = the per-piece sums between the two launches of PageRank.java:139's
+ * replacement, "col16", "col", "bits", "roffL", "x", "maps", "meta") to a fresh device
+ * allocation -- new buffer, device copy, old one freed.  Results do not change; the round's time
+ * can: the stream launch's rate depends on which physical memory the partial array occupies
+ * (scripts/probes/placement_probe.cpp).  PR_CONTIG=1 asks for a physically contiguous buffer,
+ * PR_VMM_MB=m for a virtual range backed by separately created m-MB chunks. */
+int pr_debug_move_array(pr_ctx* ctx, const char* name);
 int pr_comm_query(pr_ctx* ctx, int32_t* transport, int32_t* comm_ranks, int32_t* comm_rank);
 
 /* The engine's partitioner, on the host.  Spark's HashPartitioner decides which executor owns

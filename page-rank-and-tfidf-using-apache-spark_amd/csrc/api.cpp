@@ -1443,6 +1443,18 @@ int pr_layout_map(int32_t n_ranks, int32_t rank, uint32_t n_a, uint32_t n_b, uin
                                local_row_out, x_pos_out, dims_out);
 }
 
+int pr_debug_move_array(pr_ctx* c, const char* name) {
+  int rc = need_device(c);
+  if (rc) return rc;
+  rc = need_graph(c);
+  if (rc) return rc;
+  HIPCHK(c, hipDeviceSynchronize());
+  std::string e;
+  rc = prmi::dev_move_array(&c->dg, name, &e);
+  if (rc) return fail(c, rc, "move array: " + e);
+  return PR_OK;
+}
+
 int pr_selftest_sum_order(pr_ctx* c, uint32_t cases, uint32_t launches, uint64_t* copies,
                           uint64_t* differing, uint64_t* lane_order_cases) {
   int rc = need_device(c);

@@ -353,6 +353,11 @@ int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s,
 int host_layout_map(int p, int rank, uint32_t nA, uint32_t nB, uint32_t nC, uint64_t cnt,
                     const uint32_t* k, uint32_t* owner, uint32_t* local, uint64_t* xp,
                     uint64_t dims[4]);
+// Placement experiment: move one of the round's arrays ("partial", "col16", "col", "bits",
+// "roffL", "x", "maps", "meta") to a fresh allocation (new buffer, device copy, old one freed).
+// PR_CONTIG=1: the new buffer is physically contiguous; PR_VMM_MB=m: it is a virtual range
+// backed by separately created m-MB chunks.
+int dev_move_array(DevGraph* g, const char* name, std::string* err);
 // A one-wave kernel that sleeps ~us microseconds on stream s (exchange measurements only).
 int dev_delay_us(int us, hipStream_t s);
 int dev_selftest_lds_order(uint32_t cases, uint32_t launches, hipStream_t s, uint64_t* copies,

@@ -3515,6 +3515,85 @@ int dev_topk_candidates(DevGraph* g, uint64_t k, std::vector<uint32_t>* ids,
 
 // One wave that sleeps for about `us` microseconds (s_memrealtime ticks at 100 MHz); bounded by
 // an iteration cap, so it ends whatever the clock does.  Measurements only.
+// a virtual range of `size` bytes backed by separately created chunks of `chunk` bytes
+static int vmm_alloc(void** out, size_t size, size_t chunk, std::string* err) {
+  int dev = 0;
+  HIPTRY(hipGetDevice(&dev));
+  hipMemAllocationProp prop{};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  size_t gran = 0;
+  HIPTRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+  chunk = (chunk + gran - 1) / gran * gran;
+  const size_t total = (size + chunk - 1) / chunk * chunk;
+  void* va = nullptr;
+  HIPTRY(hipMemAddressReserve(&va, total, chunk, nullptr, 0));
+  for (size_t off = 0; off < total; off += chunk) {
+    hipMemGenericAllocationHandle_t h;
+    HIPTRY(hipMemCreate(&h, chunk, &prop, 0));
+    HIPTRY(hipMemMap(static_cast<char*>(va) + off, chunk, 0, h, 0));
+  }
+  hipMemAccessDesc d{};
+  d.location = prop.location;
+  d.flags = hipMemAccessFlagsProtReadWrite;
+  HIPTRY(hipMemSetAccess(va, total, &d, 1));
+  *out = va;
+  return PR_OK;
+}
+
+int dev_move_array(DevGraph* g, const char* name, std::string* err) {
+  const std::string nm = name ? name : "";
+  auto move = [&](auto** pp) -> int {
+    if (!*pp) return PR_OK;
+    void* base = nullptr;
+    size_t size = 0;
+    HIPTRY(hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t*>(&base), &size, reinterpret_cast<hipDeviceptr_t>(*pp)));
+    if (base != static_cast<void*>(*pp)) {
+      if (err) *err = "array is not the start of its allocation";
+      return PR_E_ARG;
+    }
+    void* fresh = nullptr;
+    const int vmm_mb = env_int("PR_VMM_MB", 0);
+    if (vmm_mb > 0) {
+      int rc = vmm_alloc(&fresh, size, static_cast<size_t>(vmm_mb) << 20, err);
+      if (rc) return rc;
+    } else if (env_int("PR_CONTIG", 0)) {
+      HIPTRY(hipExtMallocWithFlags(&fresh, size, hipDeviceMallocContiguous));
+    } else {
+      HIPTRY(hipMalloc(&fresh, size));
+    }
+    HIPTRY(hipMemcpy(fresh, *pp, size, hipMemcpyDeviceToDevice));
+    if (env_int("PR_VERBOSE", 0))
+      fprintf(stderr, "[move] %s: %p -> %p (%.1f MB) | col16 %p col %p bits %p x %p %p\n", nm.c_str(), static_cast<void*>(*pp), fresh,
+              size / 1048576.0, static_cast<void*>(g->col16), static_cast<void*>(g->col), static_cast<void*>(g->bits),
+              static_cast<void*>(g->xbuf[0]), static_cast<void*>(g->xbuf[1]));
+    HIPTRY(hipFree(*pp));
+    *pp = static_cast<std::remove_reference_t<decltype(**pp)>*>(fresh);
+    return PR_OK;
+  };
+  int rc = PR_OK;
+  if (nm == "partial") rc = move(&g->partial);
+  else if (nm == "col16") rc = move(&g->col16);
+  else if (nm == "col") rc = move(&g->col);
+  else if (nm == "bits") rc = move(&g->bits);
+  else if (nm == "roffL") rc = move(&g->roffL);
+  else if (nm == "meta") rc = move(&g->meta);
+  else if (nm == "x") {
+    rc = move(&g->xbuf[0]);
+    if (!rc) rc = move(&g->xbuf[1]);
+    if (!rc) rc = move(&g->x_init);
+  } else if (nm == "maps") {
+    rc = move(&g->nebase);
+    if (!rc) rc = move(&g->lfirst);
+    if (!rc) rc = move(&g->lmask);
+  } else {
+    if (err) *err = "unknown array";
+    return PR_E_ARG;
+  }
+  return rc;
+}
+
 __global__ void k_delay(uint32_t ticks) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t i = 0; i < (1u << 22); ++i) {
