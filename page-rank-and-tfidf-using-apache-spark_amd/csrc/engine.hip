@@ -3528,12 +3528,22 @@ static int vmm_alloc(void** out, size_t size, size_t chunk, std::string* err) {
   chunk = (chunk + gran - 1) / gran * gran;
   const size_t total = (size + chunk - 1) / chunk * chunk;
   void* va = nullptr;
-  HIPTRY(hipMemAddressReserve(&va, total, chunk, nullptr, 0));
+  HIPTRY(hipMemAddressReserve(&va, total, gran, nullptr, 0));
+  // PR_VMM_GAP_GB=g: g GB of device memory are skipped between consecutive chunks (held by
+  // allocations that are released once every chunk exists), so the chunks spread over the device
+  const size_t gap = static_cast<size_t>(std::max(0, env_int("PR_VMM_GAP_GB", 0))) << 30;
+  std::vector<void*> spacers;
   for (size_t off = 0; off < total; off += chunk) {
     hipMemGenericAllocationHandle_t h;
     HIPTRY(hipMemCreate(&h, chunk, &prop, 0));
     HIPTRY(hipMemMap(static_cast<char*>(va) + off, chunk, 0, h, 0));
+    if (gap && off + chunk < total) {
+      void* sp = nullptr;
+      if (hipMalloc(&sp, gap) == hipSuccess) spacers.push_back(sp);
+      else (void)hipGetLastError();
+    }
   }
+  for (void* sp : spacers) (void)hipFree(sp);
   hipMemAccessDesc d{};
   d.location = prop.location;
   d.flags = hipMemAccessFlagsProtReadWrite;
