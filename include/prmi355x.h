@@ -178,7 +178,7 @@ int pr_selftest_sum_order(pr_ctx* ctx, uint32_t cases, uint32_t launches, uint64
  * allocation -- new buffer, device copy, old one freed.  Results do not change; the round's time
  * can: the stream launch's rate depends on which physical memory the partial array occupies
  * (scripts/probes/placement_probe.cpp).  PR_CONTIG=1 asks for a physically contiguous buffer,
- * PR_VMM_MB=m for a virtual range backed by separately created m-MB chunks (PR_VMM_GAP_GB=g:
+ * PR_VMM_MB=m / PR_VMM_KB=k for a virtual range backed by separately created chunks (PR_VMM_GAP_GB=g:
  * g GB of device memory skipped between consecutive chunks). */
 int pr_debug_move_array(pr_ctx* ctx, const char* name);
 int pr_comm_query(pr_ctx* ctx, int32_t* transport, int32_t* comm_ranks, int32_t* comm_rank);

@@ -3524,7 +3524,9 @@ static int vmm_alloc(void** out, size_t size, size_t chunk, std::string* err) {
   prop.location.type = hipMemLocationTypeDevice;
   prop.location.id = dev;
   size_t gran = 0;
-  HIPTRY(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+  HIPTRY(hipMemGetAllocationGranularity(&gran, &prop, chunk < (2u << 20) ? hipMemAllocationGranularityMinimum
+                                                                            : hipMemAllocationGranularityRecommended));
+  if (env_int("PR_VERBOSE", 0)) fprintf(stderr, "[vmm] granularity %zu, chunk %zu\n", gran, chunk);
   chunk = (chunk + gran - 1) / gran * gran;
   const size_t total = (size + chunk - 1) / chunk * chunk;
   void* va = nullptr;
@@ -3564,9 +3566,9 @@ int dev_move_array(DevGraph* g, const char* name, std::string* err) {
       return PR_E_ARG;
     }
     void* fresh = nullptr;
-    const int vmm_mb = env_int("PR_VMM_MB", 0);
-    if (vmm_mb > 0) {
-      int rc = vmm_alloc(&fresh, size, static_cast<size_t>(vmm_mb) << 20, err);
+    const int vmm_mb = env_int("PR_VMM_MB", 0), vmm_kb = env_int("PR_VMM_KB", 0);
+    if (vmm_mb > 0 || vmm_kb > 0) {
+      int rc = vmm_alloc(&fresh, size, vmm_kb > 0 ? static_cast<size_t>(vmm_kb) << 10 : static_cast<size_t>(vmm_mb) << 20, err);
       if (rc) return rc;
     } else if (env_int("PR_CONTIG", 0)) {
       HIPTRY(hipExtMallocWithFlags(&fresh, size, hipDeviceMallocContiguous));
