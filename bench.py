@@ -280,6 +280,12 @@ def main():
                          "comm_rank": comm["comm_rank"],
                          "exposed_ms_per_rank": exposed_rank},
             "build_s": round(build_s, 2),
+            # the build may move the per-piece sums to faster physical memory (PR_PLACE=0: off):
+            # placements it timed beyond the first, stream launch with the first and with the
+            # one it kept (rank 0)
+            "placement": {"tried": int(info.get("place_tried", 0)),
+                          "stream_ms_first": round(info.get("place_ms_first", 0.0), 4),
+                          "stream_ms_kept": round(info.get("place_ms_best", 0.0), 4)},
             "build_id": P.build_id(),
         }
         print(json.dumps(line), flush=True)

@@ -101,7 +101,10 @@ typedef struct {
   double ms_build;        /* device CSR build                                             */
   uint64_t ingest_flags;  /* bit 0: the text was parsed on the host because it does not fit
                              the device ingest (>= 2^30 id tokens or device memory)         */
-  uint64_t reserved[5];
+  uint64_t place_tried;   /* placements of the per-piece sums the build timed beyond the first */
+  double place_ms_first;  /* stream launch with the array as first allocated, 0 = not timed   */
+  double place_ms_best;   /* ... and with the placement the build kept                        */
+  uint64_t reserved[2];
 } pr_graph_info;
 
 /* Library version "major.minor". */

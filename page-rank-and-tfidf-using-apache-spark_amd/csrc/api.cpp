@@ -1129,6 +1129,9 @@ int pr_graph_get_info(pr_ctx* c, pr_graph_info* o) {
     o->local_rows = c->dg.lrows;
     o->local_nnz = c->dg.lnnz;
     o->ms_build = c->dg.ms_build;
+    o->place_tried = static_cast<uint64_t>(c->dg.place_tried);
+    o->place_ms_first = c->dg.place_ms_first;
+    o->place_ms_best = c->dg.place_ms_best;
   }
   return PR_OK;
 }

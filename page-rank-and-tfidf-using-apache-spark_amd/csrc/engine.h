@@ -107,6 +107,8 @@ struct Tuning {
   int stream_cus = 32;  // PR_STREAM_CUS: stream workgroups (= compute units) per XCD; 31 at p > 1
   int l2late = 0;       // PR_L2LATE: L2-role waves prefetch the next task's columns after
                         // their gathers instead of before (see StreamArgs::l2late)
+  int place = 1;        // PR_PLACE: the build may move the partial array to faster memory
+                        // (dev_tune_placement); PR_PLACE_MIN_MB [1024]: arrays below stay put
   int lean = 1;         // PR_LEAN: 1 = the lean per-task instruction stream of the stream launch
                         // (fma-form piece sums, DPP-masked scans, SDWA LDS addresses: -11 %
                         // VALU instructions, time unchanged), 0 = the earlier form; both
@@ -214,6 +216,10 @@ struct DevGraph {
   double* dp_out = nullptr;        // [64 * dp_groups] the sums (a side array: not the ranks)
   uint32_t dp_groups = 0;
   bool no_alloc = false;           // inside pr_run_static: nothing may allocate (no PR_STAMPS)
+  // dev_tune_placement: placements timed beyond the first, stream launch with the first and
+  // with the chosen one
+  int place_tried = 0;
+  double place_ms_first = 0, place_ms_best = 0;
   Tuning tune;
 };
 
@@ -353,6 +359,13 @@ int dev_export_csr(DevGraph* g, uint64_t* row_ptr, uint32_t* col, hipStream_t s,
 int host_layout_map(int p, int rank, uint32_t nA, uint32_t nB, uint32_t nC, uint64_t cnt,
                     const uint32_t* k, uint32_t* owner, uint32_t* local, uint64_t* xp,
                     uint64_t dims[4]);
+// The stream launch's rate depends on which physical memory holds the partial array: the same
+// kernels on the same graph run the launch in 1.55 or in 1.67 ms (R-MAT scale 26), for as long
+// as the allocation lives.  The build therefore times the launch with a few more placements of
+// the array -- each allocated while other device memory is held, which is released again before
+// the timing -- keeps the fastest and frees the others.  Best effort: an allocation that fails
+// ends the search, never the build.
+int dev_tune_placement(DevGraph* g, hipStream_t s);
 // Placement experiment: move one of the round's arrays ("partial", "col16", "col", "bits",
 // "roffL", "x", "maps", "meta") to a fresh allocation (new buffer, device copy, old one freed).
 // PR_CONTIG=1: the new buffer is physically contiguous; PR_VMM_MB=m: it is a virtual range

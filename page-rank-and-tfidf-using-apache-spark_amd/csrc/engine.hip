@@ -2805,6 +2805,8 @@ int dev_build(DevGraph* g, const BuildInput& in, hipStream_t s, std::string* err
   HIPTRY(hipStreamSynchronize(s));
   HIPTRY(hipGetLastError());
   g->built = true;
+  span.next("prmi:build:placement");
+  (void)dev_tune_placement(g, s);
   g->ms_build = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return PR_OK;
 }
@@ -3221,6 +3223,119 @@ int dev_round_single(DevGraph* g, int t, int mode, bool tracked, hipStream_t s, 
 // Exchange plan of the chunked x' exchange (p > 1): chunk k covers the slot positions
 // [P_{k-1}, P_k) of every slice sub-region of a rank's slot (the same on every rank), and the
 // class-A row blocks [b0, b1) that write them on this rank.
+int dev_tune_placement(DevGraph* g, hipStream_t s) {
+  g->place_tried = 0;
+  g->place_ms_first = g->place_ms_best = 0;
+  const size_t bytes = 8ull * g->n_pieces;
+  const size_t min_bytes = static_cast<size_t>(std::max(1, env_int("PR_PLACE_MIN_MB", 1024))) << 20;
+  // (small graphs run from the caches; the PR_DBG timing switches may leave pieces unwritten)
+  if (env_int("PR_PLACE", g->tune.place) <= 0 || !g->partial || !g->ntask || !g->nlds || bytes < min_bytes || g->tune.dbg)
+    return PR_OK;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return PR_OK;
+  const size_t keep = 16ull << 30;  // left alone for the caller
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return PR_OK;
+  const bool na = g->no_alloc;
+  g->no_alloc = true;  // (no PR_STAMPS dump from these launches)
+  // the search may take this long (holding memory means clearing it first: up to 30 ms per GB)
+  const auto t_begin = std::chrono::steady_clock::now();
+  const double budget_ms = std::max(0, env_int("PR_PLACE_BUDGET_MS", 1200));
+  auto spent = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count(); };
+  // the stream launch's time with the current array: pairs of launches until three pairs in a
+  // row agree to 1 % (memory released just before is still being cleared in the background)
+  auto measure = [&](float* out) -> bool {
+    float h[3] = {-1.f, -1.f, -1.f};
+    for (int it = 0; it < 60; ++it) {
+      float ms = 0.f;
+      bool ok = hipEventRecord(e0, s) == hipSuccess;
+      for (int r = 0; r < 2 && ok; ++r) ok = dev_round_stream(g, 1, s, nullptr, 0) == PR_OK;
+      ok = ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+           hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+      if (!ok) return false;
+      h[0] = h[1];
+      h[1] = h[2];
+      h[2] = 0.5f * ms;
+      if (h[0] > 0.f) {
+        const float lo = std::min(h[0], std::min(h[1], h[2])), hi = std::max(h[0], std::max(h[1], h[2]));
+        if (hi <= 1.01f * lo) break;
+      }
+    }
+    *out = std::min(h[2], h[1] > 0.f ? h[1] : h[2]);
+    return true;
+  };
+  // a candidate: the array allocated while other device memory is held, which is released again
+  // before the launch is timed.  kind 0: G GB in 1-GB blocks; kind 1: one block of G GB that has
+  // been allocated and released once before
+  auto candidate = [&](int kind, size_t G) -> double* {
+    if (fr < keep + bytes + (G << 30)) return nullptr;
+    std::vector<void*> held;
+    bool whole = true;
+    if (kind == 0) {
+      for (size_t i = 0; i < G; ++i) {
+        void* b = nullptr;
+        if (spent() > budget_ms || hipMalloc(&b, 1ull << 30) != hipSuccess) {
+          whole = false;
+          break;
+        }
+        held.push_back(b);
+      }
+    } else {
+      void* b = nullptr;
+      if (hipMalloc(&b, G << 30) == hipSuccess) {
+        (void)hipFree(b);
+        b = nullptr;
+        if (hipMalloc(&b, G << 30) == hipSuccess) held.push_back(b);
+      }
+    }
+    void* c = nullptr;
+    if (!whole || hipMalloc(&c, bytes) != hipSuccess) c = nullptr;
+    for (void* b : held) (void)hipFree(b);
+    (void)hipGetLastError();
+    return static_cast<double*>(c);
+  };
+  float first = 0.f, best = 0.f;
+  double* best_p = g->partial;
+  if (measure(&first)) {
+    best = first;
+    // (on a box that has run nothing yet the first of these is the fast one)
+    const struct { int kind; size_t G; } plan[] = {{0, 64}, {0, 96}, {1, 48}};
+    for (const auto& pl : plan) {
+      if (spent() > budget_ms) break;
+      double* c = candidate(pl.kind, pl.G);
+      if (!c) continue;
+      g->partial = c;
+      float ms = 0.f;
+      const bool ok = measure(&ms);
+      ++g->place_tried;
+      (void)hipStreamSynchronize(s);
+      if (ok && ms < best) {
+        (void)hipFree(best_p);
+        best_p = c;
+        best = ms;
+      } else {
+        (void)hipFree(c);
+      }
+      g->partial = best_p;
+      if (env_int("PR_VERBOSE", 0) > 1)
+        fprintf(stderr, "[prmi355x] placement kind %d behind %zu GB: stream launch %.3f ms\n", pl.kind, pl.G, ms);
+      if (!ok || best < 0.955f * first) break;  // (two rates, 7 % apart: the fast one has been found)
+    }
+  }
+  (void)hipGetLastError();
+  (void)hipStreamSynchronize(s);
+  g->partial = best_p;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  g->no_alloc = na;
+  g->place_ms_first = first;
+  g->place_ms_best = best;
+  if (env_int("PR_VERBOSE", 0))
+    fprintf(stderr, "[prmi355x] placement of the partial array: stream launch %.3f ms as built, %.3f ms chosen after %d more placements\n",
+            first, best, g->place_tried);
+  return PR_OK;
+}
+
 bool dev_can_split_stream(const DevGraph* g) {
   // the hot prefix of a slice's q-space is a prefix of every slot sub-region only in the
   // slice-major x layout, and a split needs LDS blocks (the two-role stream kernel)

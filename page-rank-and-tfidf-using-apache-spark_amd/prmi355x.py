@@ -88,7 +88,9 @@ class GraphInfo(C.Structure):
                 ("dangling_entries", C.c_uint64), ("n_sources", C.c_uint64),
                 ("n_rows", C.c_uint64), ("local_rows", C.c_uint64), ("local_nnz", C.c_uint64),
                 ("ms_ingest", C.c_double), ("ms_build", C.c_double),
-                ("ingest_flags", C.c_uint64), ("reserved", C.c_uint64 * 5)]
+                ("ingest_flags", C.c_uint64), ("place_tried", C.c_uint64),
+                ("place_ms_first", C.c_double), ("place_ms_best", C.c_double),
+                ("reserved", C.c_uint64 * 2)]
 
     def as_dict(self) -> Dict[str, float]:
         return {k: getattr(self, k) for k, _t in self._fields_ if k != "reserved"}

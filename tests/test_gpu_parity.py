@@ -489,3 +489,24 @@ def test_rank_sum_checksum_scale22(P):
     assert st["rank_sum"] == math.fsum(r.tolist())
     d = r > 0
     assert d.sum() > 0 and np.all(r[d] >= 0.15)
+
+
+def test_placement_search_changes_no_bits(P, monkeypatch):
+    """The build may move the per-piece sums to another allocation when the stream launch runs
+    faster there (dev_tune_placement; large graphs only unless PR_PLACE_MIN_MB says otherwise).
+    Where the array lives changes no sum: ranks with the search on and off are bit-identical,
+    and the graph info reports what the search timed."""
+    monkeypatch.setenv("PR_PLACE_MIN_MB", "1")
+    monkeypatch.setenv("PR_PLACE_BUDGET_MS", "400")
+    out = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("PR_PLACE", on)
+        eng = P.Engine(device=0)
+        eng.generate_rmat(20, 16, 11)
+        info = eng.info()
+        eng.run(6)
+        out.append((eng.ranks(), info))
+        eng.close()
+    assert np.array_equal(out[0][0].view(np.uint64), out[1][0].view(np.uint64))
+    assert out[0][1]["place_ms_first"] > 0 and out[0][1]["place_ms_best"] <= out[0][1]["place_ms_first"]
+    assert out[1][1]["place_ms_first"] == 0 and out[1][1]["place_tried"] == 0
