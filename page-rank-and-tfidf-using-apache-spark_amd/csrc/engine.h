@@ -363,7 +363,8 @@ int host_layout_map(int p, int rank, uint32_t nA, uint32_t nB, uint32_t nC, uint
 // kernels on the same graph run the launch in 1.55 or in 1.67 ms (R-MAT scale 26), for as long
 // as the allocation lives.  The build therefore times the launch with a few more placements of
 // the array -- each allocated while other device memory is held, which is released again before
-// the timing -- keeps the fastest and frees the others.  Best effort: an allocation that fails
+// the timing -- keeps the fastest and frees the others; then the same for the LDS groups' column
+// stream, the largest array the launch reads (2 % more).  Best effort: an allocation that fails
 // ends the search, never the build.
 int dev_tune_placement(DevGraph* g, hipStream_t s);
 // Placement experiment: move one of the round's arrays ("partial", "col16", "col", "bits",

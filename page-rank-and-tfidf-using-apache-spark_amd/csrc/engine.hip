@@ -3240,7 +3240,7 @@ int dev_tune_placement(DevGraph* g, hipStream_t s) {
   g->no_alloc = true;  // (no PR_STAMPS dump from these launches)
   // the search may take this long (holding memory means clearing it first: up to 30 ms per GB)
   const auto t_begin = std::chrono::steady_clock::now();
-  const double budget_ms = std::max(0, env_int("PR_PLACE_BUDGET_MS", 1200));
+  const double budget_ms = std::max(0, env_int("PR_PLACE_BUDGET_MS", 1600));
   auto spent = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count(); };
   // the stream launch's time with the current array: pairs of launches until three pairs in a
   // row agree to 1 % (memory released just before is still being cleared in the background)
@@ -3264,11 +3264,11 @@ int dev_tune_placement(DevGraph* g, hipStream_t s) {
     *out = std::min(h[2], h[1] > 0.f ? h[1] : h[2]);
     return true;
   };
-  // a candidate: the array allocated while other device memory is held, which is released again
+  // a candidate: `bytes` allocated while other device memory is held, which is released again
   // before the launch is timed.  kind 0: G GB in 1-GB blocks; kind 1: one block of G GB that has
   // been allocated and released once before
-  auto candidate = [&](int kind, size_t G) -> double* {
-    if (fr < keep + bytes + (G << 30)) return nullptr;
+  auto candidate = [&](int kind, size_t G, size_t nbytes) -> void* {
+    if (fr < keep + nbytes + (G << 30)) return nullptr;
     std::vector<void*> held;
     bool whole = true;
     if (kind == 0) {
@@ -3289,50 +3289,65 @@ int dev_tune_placement(DevGraph* g, hipStream_t s) {
       }
     }
     void* c = nullptr;
-    if (!whole || hipMalloc(&c, bytes) != hipSuccess) c = nullptr;
+    if (!whole || hipMalloc(&c, nbytes) != hipSuccess) c = nullptr;
     for (void* b : held) (void)hipFree(b);
     (void)hipGetLastError();
-    return static_cast<double*>(c);
+    return c;
   };
-  float first = 0.f, best = 0.f;
-  double* best_p = g->partial;
-  if (measure(&first)) {
-    best = first;
-    // (on a box that has run nothing yet the first of these is the fast one)
-    const struct { int kind; size_t G; } plan[] = {{0, 64}, {0, 96}, {1, 48}};
-    for (const auto& pl : plan) {
+  struct Plan { int kind; size_t G; };
+  // the search for one array: `slot` points at the engine's pointer to it; `copy`: it holds data
+  // (the partial array is rewritten by every launch, the column stream is not); a candidate
+  // replaces the current placement when it is faster, the search ends when one is faster than
+  // `stop` x the first timing
+  auto search = [&](void** slot, size_t nbytes, bool copy, float first_ms, float stop, std::initializer_list<Plan> plan) -> float {
+    float best_ms = first_ms;
+    for (const Plan& pl : plan) {
       if (spent() > budget_ms) break;
-      double* c = candidate(pl.kind, pl.G);
+      void* c = candidate(pl.kind, pl.G, nbytes);
       if (!c) continue;
-      g->partial = c;
+      void* prev = *slot;
+      if (copy && hipMemcpyAsync(c, prev, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+        (void)hipFree(c);
+        break;
+      }
+      *slot = c;
       float ms = 0.f;
       const bool ok = measure(&ms);
       ++g->place_tried;
       (void)hipStreamSynchronize(s);
-      if (ok && ms < best) {
-        (void)hipFree(best_p);
-        best_p = c;
-        best = ms;
+      if (ok && ms < best_ms) {
+        (void)hipFree(prev);
+        best_ms = ms;
       } else {
+        *slot = prev;
         (void)hipFree(c);
       }
-      g->partial = best_p;
       if (env_int("PR_VERBOSE", 0) > 1)
-        fprintf(stderr, "[prmi355x] placement kind %d behind %zu GB: stream launch %.3f ms\n", pl.kind, pl.G, ms);
-      if (!ok || best < 0.955f * first) break;  // (two rates, 7 % apart: the fast one has been found)
+        fprintf(stderr, "[prmi355x] placement kind %d behind %zu GB (%.1f GB array): stream launch %.3f ms\n", pl.kind, pl.G,
+                nbytes / 1073741824.0, ms);
+      if (!ok || best_ms < stop * first_ms) break;
     }
+    return best_ms;
+  };
+  float first = 0.f, best = 0.f;
+  if (measure(&first)) {
+    // the partial array: two rates, 7 % apart -- stop at the first candidate that has the fast
+    // one (on a box that has run nothing yet that is one of the first two)
+    best = search(reinterpret_cast<void**>(&g->partial), bytes, false, first, 0.955f, {{0, 64}, {0, 96}, {1, 48}});
+    // the LDS groups' column stream, the largest array the launch reads: worth 2 % more
+    const size_t cbytes = 2ull * g->n_col16;
+    if (g->col16 && cbytes >= min_bytes) best = search(reinterpret_cast<void**>(&g->col16), cbytes, true, best, 0.985f, {{0, 64}, {0, 96}});
   }
   (void)hipGetLastError();
   (void)hipStreamSynchronize(s);
-  g->partial = best_p;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   g->no_alloc = na;
   g->place_ms_first = first;
   g->place_ms_best = best;
   if (env_int("PR_VERBOSE", 0))
-    fprintf(stderr, "[prmi355x] placement of the partial array: stream launch %.3f ms as built, %.3f ms chosen after %d more placements\n",
-            first, best, g->place_tried);
+    fprintf(stderr, "[prmi355x] placement of the partial array and the column stream: stream launch %.3f ms as built, %.3f ms chosen after %d more placements (%.1f of %.1f GB free, %.0f ms)\n",
+            first, best, g->place_tried, fr / 1073741824.0, tot / 1073741824.0, spent());
   return PR_OK;
 }
 
