@@ -3332,11 +3332,11 @@ int dev_tune_placement(DevGraph* g, hipStream_t s) {
   float first = 0.f, best = 0.f;
   if (measure(&first)) {
     // the partial array: two rates, 7 % apart -- stop at the first candidate that has the fast
-    // one (on a box that has run nothing yet that is one of the first two)
-    best = search(reinterpret_cast<void**>(&g->partial), bytes, false, first, 0.955f, {{0, 64}, {0, 96}, {1, 48}});
+    // one (on a box that has run nothing yet that is, most often, the first)
+    best = search(reinterpret_cast<void**>(&g->partial), bytes, false, first, 0.955f, {{0, 96}, {0, 64}, {1, 48}});
     // the LDS groups' column stream, the largest array the launch reads: worth 2 % more
     const size_t cbytes = 2ull * g->n_col16;
-    if (g->col16 && cbytes >= min_bytes) best = search(reinterpret_cast<void**>(&g->col16), cbytes, true, best, 0.985f, {{0, 64}, {0, 96}});
+    if (g->col16 && cbytes >= min_bytes) best = search(reinterpret_cast<void**>(&g->col16), cbytes, true, best, 0.985f, {{0, 96}, {0, 64}});
   }
   (void)hipGetLastError();
   (void)hipStreamSynchronize(s);
