@@ -12,6 +12,11 @@ for p in (PKG, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# The build's placement search (large graphs only) is a matter of speed, not of results: the
+# tests give it a short budget so the scale-26 / scale-28 cases do not pay seconds per build
+# (test_placement_search_changes_no_bits sets its own).
+os.environ.setdefault("PR_PLACE_BUDGET_MS", "300")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD MI355X (run with -m gpu)")
