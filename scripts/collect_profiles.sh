@@ -13,7 +13,7 @@ pass() { # name, rocprof args...
   [ $rc -eq 0 ] || exit $rc
 }
 BA=("$@")
-pass kt --kernel-trace --stats
+[ -n "$SKIP_KT" ] || pass kt --kernel-trace --stats   # (SKIP_KT: the caller has taken the trace already)
 pass rd --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --kernel-include-regex spmv
 pass wr --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-include-regex spmv
 pass fetch --pmc FETCH_SIZE --kernel-include-regex spmv
