@@ -2933,6 +2933,7 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   if (!lattr) {
     for (const void* f : {reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 0>),
                           reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 32>),
+                          reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, 8>),
                           reinterpret_cast<const void*>(&spmv_stream<2, true, false, 0, true, EXP_ALL>),
                           reinterpret_cast<const void*>(&spmv_stream<2, true, true, 0, true>),
                           reinterpret_cast<const void*>(&spmv_stream<0, true, false, 0, true>)})
@@ -2941,7 +2942,9 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   }
   // what the launch needs of the kernel beyond the plain single-rank form (see EXP)
   const bool want_dyn = A.gcnt != nullptr && (A.dyn0 < A.nlds || A.l2dyn != 0u);
-  const int feat = (want_dyn || A.early != 0u) ? EXP_ALL : (A.part != 0u ? 32 : 0);
+  // (slice-wide claims alone, on an uncut launch, have an instantiation of their own)
+  const int feat = (want_dyn && A.early == 0u && A.part == 0u) ? 8
+                   : ((want_dyn || A.early != 0u) ? EXP_ALL : (A.part != 0u ? 32 : 0));
   const int exper = g->tune.l2late == 1 ? 1 : (g->tune.l2late == 2 ? 2 : ((g->tune.dbg & (8192 | 16384)) ? 4 : 0));
   // (PR_DBG=16384 runs the PR_DBG=8192 instantiation with its fast path off: that variant
   // carries 22 spilled registers, so its A/B partner must carry them too)
@@ -2964,6 +2967,7 @@ void launch_stream(const DevGraph* g, const StreamArgs& A, hipStream_t s) {
   else if (split && st && lean) hipLaunchKernelGGL((spmv_stream<2, true, true, 0, true>), gr, bl, lds, s, A);
   else if (split && lean && feat == EXP_ALL) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, EXP_ALL>), gr, bl, lds, s, A);
   else if (split && lean && feat == 32) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, 32>), gr, bl, lds, s, A);
+  else if (split && lean && feat == 8) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, 8>), gr, bl, lds, s, A);
   else if (split && lean) hipLaunchKernelGGL((spmv_stream<2, true, false, 0, true, 0>), gr, bl, lds, s, A);
   else if (split && st) hipLaunchKernelGGL((spmv_stream<2, true, true>), gr, bl, lds, s, A);
   else if (split) hipLaunchKernelGGL((spmv_stream<2, true, false>), gr, bl, lds, s, A);
